@@ -1,0 +1,52 @@
+/*
+ * klb_imageIO.h -- encode/decode engine of the .lfm container.
+ *
+ * Same public surface as the reference class (src/klb_imageIO.h:47-135) so
+ * the MEX sources in matlabWrapper/ relink unchanged: public `header` and
+ * `numThreads`, writeImage / writeImageStackSlices / readImage /
+ * readImageFull / readHeader.  The implementation is MI355X-native: the
+ * predictor stage and the predictor selection run as HIP kernels on the GPU
+ * (lfm_hip.h) for whole stacks at once; bzip2 runs on a host worker pool
+ * with an in-order writer.
+ */
+#ifndef LFM_KLB_IMAGE_IO_H
+#define LFM_KLB_IMAGE_IO_H
+
+#include <string>
+#include <cstdint>
+#include "klb_imageHeader.h"
+#include "klb_ROI.h"
+
+class __attribute__((visibility("default"))) klb_imageIO
+{
+public:
+    klb_image_header header;
+    int numThreads;
+
+    klb_imageIO();
+    explicit klb_imageIO(const std::string& filename_);
+
+    std::string getFilename() const { return filename; }
+    void setFilename(const std::string& filename_) { filename = filename_; }
+
+    int readHeader() { return header.readHeader(filename.c_str()); }
+    int readHeader(const std::string& filename_)
+    {
+        filename = filename_;
+        return readHeader();
+    }
+
+    /* Encode `img` (layout x fastest, then y, z, c, t) with the current header
+     * to getFilename().  headerVersion bits 0-6 < 8 auto-select the predictor
+     * on frame 0, 8..15 force predictor (request - 8); bit 7 = video. */
+    int writeImage(const char* img, int numThreads);
+    int writeImageStackSlices(const char** img, int numThreads);
+
+    int readImage(char* img, const klb_ROI* ROI, int numThreads);
+    int readImageFull(char* img, int numThreads);
+
+private:
+    std::string filename;
+};
+
+#endif

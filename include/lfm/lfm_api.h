@@ -1,0 +1,75 @@
+/*
+ * lfm_api.h -- liblfm extensions beyond the reference C ABI.
+ *
+ *  - lfm_set_family / lfm_get_family: the predictor family (0 tiles,
+ *    1 angle, 2 space), a compile-time constant in the reference
+ *    (src/common.h:19 LFM_PREDICTOR_WAY); default from env LFM_PREDICTOR_WAY.
+ *  - writeLFMstack_c / readLFMstack_c: the MEX writeLFMstack / readLFMstack
+ *    argument set (predictor request, Nnum, video flag) as plain C, for
+ *    ctypes / cgo / JNI callers (matlabWrapper/writeLFMstack.cpp:360-433).
+ *  - lfm_encoder_*: reusable encoder context that encodes to memory from a
+ *    host or a DEVICE-resident stack and reports per-stage timings (bench).
+ */
+#ifndef LFM_API_H
+#define LFM_API_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include "common.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LFM_API __attribute__((visibility("default")))
+
+LFM_API int lfm_set_family(int family);
+LFM_API int lfm_get_family(void);
+LFM_API const char* lfm_version(void);
+
+/* predictor_request: header bits 0-6 (0..7 auto, 8..15 forced k = request-8);
+ * video: header bit 7.  Returns the writeKLBstack codes. */
+LFM_API int writeLFMstack_c(const void* im, const char* filename, const uint32_t xyzct[KLB_DATA_DIMS],
+                            int dataType, int numThreads, const float pixelSize[KLB_DATA_DIMS],
+                            const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                            const char metadata[KLB_METADATA_SIZE], int predictor_request, int Nnum, int video);
+
+/* Decode into im (caller-allocated, getImageSizeBytes); the header fields are
+ * returned through the optional out pointers (headerVersion, Nnum). */
+LFM_API int readLFMstack_c(const char* filename, void* im, int numThreads, uint8_t* headerVersion, uint8_t* Nnum);
+
+typedef struct lfm_encode_stats {
+    double total_ms;      /* whole encode, wall clock                        */
+    double h2d_ms;        /* host -> device upload (0 for device input)      */
+    double select_ms;     /* predictor selection (kernels + sync), wall       */
+    double predict_ms;    /* predictor kernels, HIP events                    */
+    double d2h_ms;        /* symbols device -> host                           */
+    double compress_ms;   /* block compression + in-order assembly, wall      */
+    int chosen;           /* predictor written to the header (bits 0-6)       */
+    int header_version;   /* final header byte                                */
+    float entropy[8];     /* candidate entropies when auto-selected, else 0   */
+    uint64_t out_bytes;   /* size of the .lfm produced                        */
+} lfm_encode_stats;
+
+typedef struct lfm_encoder lfm_encoder;
+
+/* device < 0: current device; numThreads <= 0: host CPU share */
+LFM_API lfm_encoder* lfm_encoder_create(int device, int numThreads);
+LFM_API void lfm_encoder_destroy(lfm_encoder* enc);
+
+/* Encode a stack to an in-memory .lfm.  img_is_device != 0: `img` is a device
+ * pointer on the encoder's device.  *out stays valid until the next call on
+ * this encoder or its destruction. */
+LFM_API int lfm_encoder_encode(lfm_encoder* enc, const void* img, int img_is_device,
+                               const uint32_t xyzct[KLB_DATA_DIMS], int dataType, int headerVersion, int Nnum,
+                               const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                               const char metadata[KLB_METADATA_SIZE], const uint8_t** out, uint64_t* out_len,
+                               lfm_encode_stats* stats);
+
+/* Decode an in-memory .lfm into `img` (host, getImageSizeBytes bytes). */
+LFM_API int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

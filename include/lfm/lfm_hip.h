@@ -1,0 +1,76 @@
+/*
+ * lfm_hip.h -- extern "C" HIP shim of the LFM predictor path (gfx950).
+ *
+ * This is the internal kernel boundary the host encoder (klb_imageIO) calls;
+ * it replaces the reference's CUDA launchers and their call sites:
+ *   predictorK_{tiles,angle,space}_GPU + symbolize_GPU
+ *       (lfm_Predictors.h:16-40, called at klb_imageIO.cpp:1270-1300, :1696-1737)
+ *       -> lfm_hip_predict  (all frames of a stack in one launch, fused symbolize)
+ *   bwt_GPU + static_bwt_GPU + sum_bwt_GPU inside bwt_entropy_2D and the
+ *   candidate loop of predict_and_2DEntropy / writeImage
+ *       (lfm_Predictors.h:33-43; klb_imageIO.cpp:2030-2093, :2197-2225, :2273-2306)
+ *       -> lfm_hip_select / lfm_hip_entropy2d
+ *
+ * Conventions: plain device pointers owned by the caller, explicit stream
+ * (a hipStream_t passed as void*, NULL = default stream), asynchronous unless
+ * stated, status code return.  The caller selects the device (hipSetDevice).
+ */
+#ifndef LFM_HIP_H
+#define LFM_HIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum lfm_hip_status {
+    LFM_HIP_OK = 0,
+    LFM_HIP_EINVAL = 1,    /* bad argument                                   */
+    LFM_HIP_ERUNTIME = 2,  /* HIP runtime error (launch / alloc / copy)      */
+    LFM_HIP_ENOTINV = 3,   /* frame is not invertible (angle/space temporal) */
+    LFM_HIP_ENODEV = 4     /* no usable GPU                                  */
+};
+
+/* families: 0 = tiles ("ANGLE_AND_SPACE", LFM_PREDICTOR_WAY 0), 1 = angle, 2 = space */
+
+/* Forward predictor + symbolize for nframes consecutive frames of one volume.
+ * d_in holds frames z0 .. z0+nframes-1 (W*H uint16 each, x fastest); frame
+ * z is temporal when (video_bit & z) is odd, and then uses the raw frame z-1
+ * (d_in of the previous frame, or d_prev for the first one).  predictor 0
+ * copies the raw frames.  d_out receives uint16 symbols in the same layout. */
+int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uint16_t* d_out, int W, int H, int nframes,
+                    int T, int family, int predictor, int video_bit, int z0, void* stream);
+
+/* 2D entropy of a candidate buffer of npix uint16 symbols (450000-pixel
+ * chunks, klb_imageIO.cpp:2030-2093).  Synchronous: writes the float result
+ * (without the 0.96 raw-candidate factor) to *entropy. */
+int lfm_hip_entropy2d(const uint16_t* d_cand, uint64_t npix, float* entropy, void* stream);
+
+/* Predictor selection on one frame: builds the 8 candidates (0 = raw,
+ * k = predictor k, spatial), their 2D entropies (candidate 0 scaled by 0.96)
+ * and the reference argmin (exact ties -> highest index).  Synchronous.
+ * d_workspace may be NULL (allocated internally) or hold
+ * lfm_hip_select_workspace_bytes(W, H) bytes. */
+size_t lfm_hip_select_workspace_bytes(int W, int H);
+int lfm_hip_select(const uint16_t* d_frame, int W, int H, int T, int family, float entropy[8], int* chosen,
+                   void* d_workspace, void* stream);
+
+/* Synthetic light-field stack of SURVEY.md 8(d) (integer generator) written
+ * straight into device memory: X*Y*Z pixels of volume (c, t) = (0, t_index),
+ * global pixel index offset idx0 (for z-slabs of a larger stack). */
+int lfm_hip_synth(uint16_t* d_out, int X, int Y, int Z, int T, int t_index, uint64_t idx0, uint64_t seed,
+                  void* stream);
+
+/* number of visible HIP devices (0 when no GPU / no runtime) */
+int lfm_hip_device_count(void);
+
+/* debug switch (env LFM_FORCE_GENERIC=1): route predictor launches to the
+ * one-thread-per-pixel kernel instead of the LDS-ring kernel */
+int lfm_hip_force_generic(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

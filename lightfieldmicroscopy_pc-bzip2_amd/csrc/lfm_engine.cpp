@@ -1,0 +1,704 @@
+// lfm_engine.cpp -- MI355X-native encode / decode engine.
+//
+// Encode = predictor stage (GPU, lfm_hip.h) + block compression (host worker
+// pool, in-order sink).  The reference equivalents:
+//   writeImage               klb_imageIO.cpp:2248-2492
+//   predictor selection      :2273-2360 (8 candidates on frame 0, argmin)
+//   Predictor_both/_angle/_space :1227-1670 (one launch + 2 PCIe copies per frame)
+//   blockCompressor          :78-295    (x-fastest gather, BZ2 level rule, workFactor 30)
+//   blockWriter              :1145-1225 (in-order append, offset table rewritten at the end)
+// Here the whole stack is predicted by one kernel launch per (c,t) volume,
+// symbols come back with one D2H copy into pinned memory, and the block
+// compressors run on all host cores while the calling thread appends the
+// finished blocks in order.
+#include "lfm_engine.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <zlib.h>
+
+#include "bz2_sys.h"
+#include "lfm_cases.h"
+#include "lfm_hip.h"
+
+namespace lfm {
+
+namespace {
+using clk = std::chrono::steady_clock;
+double ms_since(clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); }
+
+int env_int(const char* name, int dflt)
+{
+    const char* e = getenv(name);
+    if (!e || !*e) return dflt;
+    return atoi(e);
+}
+
+std::atomic<int> g_family{-1};
+} // namespace
+
+int default_threads()
+{
+    int n = env_int("LFM_NUM_THREADS", 0);
+    if (n <= 0) n = env_int("OMP_NUM_THREADS", 0);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    return std::max(n, 1);
+}
+
+int current_family()
+{
+    int f = g_family.load();
+    if (f < 0) {
+        f = env_int("LFM_PREDICTOR_WAY", LFM_PREDICTOR_WAY);
+        if (f < 0 || f > 2) f = LFM_PREDICTOR_WAY;
+        g_family.store(f);
+    }
+    return f;
+}
+void set_family(int fam) { g_family.store(fam); }
+
+// ------------------------------------------------------------- block grid --
+BlockGrid::BlockGrid(const klb_image_header& h)
+{
+    nblocks = 1;
+    uint64_t s = 1;
+    for (int d = 0; d < 5; ++d) {
+        dims[d] = h.xyzct[d];
+        bs[d] = h.blockSize[d];
+        nb[d] = (uint64_t)std::ceil((float)h.xyzct[d] / (float)h.blockSize[d]);  // calculateNumBlocks
+        nblocks *= nb[d];
+        stride[d] = s;
+        s *= dims[d];
+    }
+}
+
+void BlockGrid::block(uint64_t id, uint64_t origin[5], uint64_t size[5]) const
+{
+    for (int d = 0; d < 5; ++d) {
+        const uint64_t c = id % nb[d];
+        id /= nb[d];
+        origin[d] = c * bs[d];
+        size[d] = std::min<uint64_t>(bs[d], dims[d] - origin[d]);
+    }
+}
+
+template <bool GATHER>
+static void walk_block(uint8_t* img, const BlockGrid& g, uint64_t id, size_t bpp, uint8_t* blk, size_t* nbytes)
+{
+    uint64_t o[5], s[5];
+    g.block(id, o, s);
+    const size_t row = s[0] * bpp;
+    size_t k = 0;
+    for (uint64_t t = 0; t < s[4]; ++t)
+        for (uint64_t c = 0; c < s[3]; ++c)
+            for (uint64_t z = 0; z < s[2]; ++z)
+                for (uint64_t y = 0; y < s[1]; ++y) {
+                    const uint64_t e = (o[0]) * g.stride[0] + (o[1] + y) * g.stride[1] + (o[2] + z) * g.stride[2] +
+                                       (o[3] + c) * g.stride[3] + (o[4] + t) * g.stride[4];
+                    if (GATHER) std::memcpy(blk + k, img + e * bpp, row);
+                    else std::memcpy(img + e * bpp, blk + k, row);
+                    k += row;
+                }
+    if (nbytes) *nbytes = k;
+}
+
+void gather_block(const uint8_t* img, const BlockGrid& g, uint64_t id, size_t bpp, uint8_t* dst, size_t* nbytes)
+{
+    walk_block<true>(const_cast<uint8_t*>(img), g, id, bpp, dst, nbytes);
+}
+void scatter_block(const uint8_t* blk, const BlockGrid& g, uint64_t id, size_t bpp, uint8_t* img)
+{
+    walk_block<false>(img, g, id, bpp, const_cast<uint8_t*>(blk), nullptr);
+}
+
+// ------------------------------------------------------------------ sinks --
+int FileSink::begin(const klb_image_header& h)
+{
+    vbuf_.resize(32 << 20);
+    setvbuf(f_, vbuf_.data(), _IOFBF, vbuf_.size());
+    std::vector<uint8_t> head(h.getSizeInBytes(), 0);
+    klb_image_header tmp(h);
+    std::fill(tmp.blockOffset, tmp.blockOffset + tmp.Nb, 0);
+    tmp.serialize(head.data(), head.size());
+    return std::fwrite(head.data(), 1, head.size(), f_) == head.size() ? 0 : 5;
+}
+int FileSink::append(const uint8_t* p, size_t n)
+{
+    return std::fwrite(p, 1, n, f_) == n ? 0 : 5;
+}
+int FileSink::finish(const klb_image_header& h)
+{
+    if (std::fseek(f_, (long)h.getSizeInBytesFixPortion(), SEEK_SET) != 0) return 5;
+    if (h.Nb && std::fwrite(h.blockOffset, sizeof(uint64_t), h.Nb, f_) != h.Nb) return 5;
+    std::fflush(f_);
+    return 0;
+}
+
+int MemSink::begin(const klb_image_header& h)
+{
+    out_->clear();
+    out_->resize(h.getSizeInBytes(), 0);
+    return 0;
+}
+int MemSink::append(const uint8_t* p, size_t n)
+{
+    out_->insert(out_->end(), p, p + n);
+    return 0;
+}
+int MemSink::finish(const klb_image_header& h)
+{
+    h.serialize(out_->data(), h.getSizeInBytes());
+    return 0;
+}
+
+// ------------------------------------------------------- block compression --
+static int compress_one(int ctype, uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap, uint32_t* out_len,
+                        int level)
+{
+    switch (ctype) {
+    case NONE:
+        std::memcpy(out, in, n);
+        *out_len = n;
+        return 0;
+    case BZIP2: {
+        unsigned int len = cap;
+        int rc = BZ2_bzBuffToBuffCompress((char*)out, &len, (char*)in, n, level, 0, 30);
+        *out_len = len;
+        return rc == LFM_BZ_OK ? 0 : 2;
+    }
+    case ZLIB: {
+        z_stream s;
+        std::memset(&s, 0, sizeof(s));
+        if (deflateInit(&s, Z_DEFAULT_COMPRESSION) != Z_OK) return 3;
+        s.next_in = in;
+        s.avail_in = n;
+        s.next_out = out;
+        s.avail_out = cap;
+        s.data_type = Z_BINARY;
+        int rc = deflate(&s, Z_FINISH);
+        *out_len = cap - s.avail_out;
+        deflateEnd(&s);
+        return (rc == Z_STREAM_END || rc == Z_OK) ? 0 : 3;
+    }
+    }
+    return 5;
+}
+
+static int decompress_one(int ctype, const uint8_t* in, uint32_t n, uint8_t* out, uint32_t expect)
+{
+    switch (ctype) {
+    case NONE:
+        if (n != expect) return 3;
+        std::memcpy(out, in, n);
+        return 0;
+    case BZIP2: {
+        unsigned int len = expect;
+        int rc = BZ2_bzBuffToBuffDecompress((char*)out, &len, (char*)in, n, 0, 0);
+        return (rc == LFM_BZ_OK && len == expect) ? 0 : 2;
+    }
+    case ZLIB: {
+        z_stream s;
+        std::memset(&s, 0, sizeof(s));
+        if (inflateInit(&s) != Z_OK) return 3;
+        s.next_in = const_cast<uint8_t*>(in);
+        s.avail_in = n;
+        s.next_out = out;
+        s.avail_out = expect;
+        int rc = inflate(&s, Z_FINISH);
+        const bool ok = (rc == Z_STREAM_END) && s.avail_out == 0;
+        inflateEnd(&s);
+        return ok ? 0 : 3;
+    }
+    }
+    return 5;
+}
+
+int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads)
+{
+    const BlockGrid g(h);
+    const uint64_t nblocks = g.nblocks;
+    h.resizeBlockOffset(nblocks);
+    const size_t bpp = h.getBytesPerPixel();
+    const uint32_t block_bytes = h.getBlockSizeBytes();                 // nominal (clamped) block
+    const int level = std::min(9, (int)((block_bytes + 99999) / 100000)); // klb_imageIO.cpp:108
+    uint32_t cap = block_bytes;
+    if (h.compressionType != NONE) cap = (uint32_t)std::ceil((float)block_bytes * 2.0f + 50.0f);
+    if (h.compressionType != NONE && h.compressionType != BZIP2 && h.compressionType != ZLIB) {
+        std::printf("ERROR: compression type not implemented\n");
+        return 5;
+    }
+    threads = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(threads, 1), nblocks));
+
+    std::vector<std::vector<uint8_t>> res(nblocks);
+    std::vector<uint8_t> done(nblocks, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> err{0};
+
+    auto worker = [&]() {
+        std::vector<uint8_t> in(block_bytes), out(cap);
+        for (;;) {
+            const uint64_t id = next.fetch_add(1);
+            if (id >= nblocks) break;
+            size_t n = 0;
+            gather_block(sym, g, id, bpp, in.data(), &n);
+            uint32_t len = 0;
+            int rc = err.load() ? 0 : compress_one(h.compressionType, in.data(), (uint32_t)n, out.data(), cap, &len, level);
+            if (rc) {
+                std::printf("ERROR: compressing block %llu failed (code %d)\n", (unsigned long long)id, rc);
+                int z = 0;
+                err.compare_exchange_strong(z, rc);
+                len = 0;
+            }
+            std::vector<uint8_t> v(out.data(), out.data() + len);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                res[id].swap(v);
+                done[id] = 1;
+            }
+            cv.notify_all();
+        }
+    };
+    std::vector<std::thread> pool;
+    pool.reserve(threads);
+    for (int i = 0; i < threads; ++i) pool.emplace_back(worker);
+
+    int rc = sink.begin(h);
+    uint64_t offset = 0;
+    for (uint64_t id = 0; id < nblocks; ++id) {
+        std::vector<uint8_t> blk;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return done[id] != 0; });
+            blk.swap(res[id]);
+        }
+        if (!rc && !err.load()) rc = sink.append(blk.data(), blk.size());
+        offset += blk.size();
+        h.blockOffset[id] = offset;
+    }
+    for (auto& t : pool) t.join();
+    if (err.load()) return err.load();
+    if (rc) return rc;
+    return sink.finish(h);
+}
+
+// --------------------------------------------------------------- encoder --
+Encoder::Encoder(int device) : device_(device) {}
+
+Encoder::~Encoder()
+{
+    if (gpu_ready_) {
+        (void)hipSetDevice(device_);
+        if (d_in_) (void)hipFree(d_in_);
+        if (d_sym_) (void)hipFree(d_sym_);
+        if (d_ws_) (void)hipFree(d_ws_);
+        if (h_sym_) (void)hipHostFree(h_sym_);
+        if (ev0_) (void)hipEventDestroy(ev0_);
+        if (ev1_) (void)hipEventDestroy(ev1_);
+        if (stream_) (void)hipStreamDestroy(stream_);
+    }
+}
+
+int Encoder::ensure_gpu()
+{
+    if (gpu_ready_) return 0;
+    int n = lfm_hip_device_count();
+    if (n <= 0) {
+        std::printf("ERROR: the LFM predictor stage needs a HIP GPU (gfx950) and none is visible\n");
+        return kErrNoGpu;
+    }
+    if (device_ < 0) {
+        if (hipGetDevice(&device_) != hipSuccess) device_ = 0;
+    }
+    if (device_ >= n || hipSetDevice(device_) != hipSuccess) return kErrNoGpu;
+    if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
+    (void)hipEventCreate(&ev0_);
+    (void)hipEventCreate(&ev1_);
+    gpu_ready_ = true;
+    return 0;
+}
+
+void* Encoder::dev_alloc(void*& p, size_t& cap, size_t need)
+{
+    if (need <= cap && p) return p;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, need) != hipSuccess) return nullptr;
+    cap = need;
+    return p;
+}
+
+int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym,
+                             lfm_encode_stats* st)
+{
+    const size_t bpp = h.getBytesPerPixel();
+    const uint8_t hv = h.headerVersion;
+    const int req = hv & 0x7F;
+    const int video = (hv >> 7) & 1;
+    const uint64_t W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
+    const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
+    const uint64_t vol = W * H * Z;
+    const uint64_t total_bytes = h.getImageSizeBytes();
+    const bool autosel = req < NUM_PREDICTORS;
+    int k = autosel ? 0 : (hv & 0x77);  // `headerVersion & 0x7F - 8` parses as & 0x77 (klb_imageIO.cpp:2380)
+    if (st) st->chosen = 0;
+
+    auto host_symbols_from_device = [&](const void* d, size_t bytes) -> int {
+        if (!h_sym_ || h_sym_cap_ < bytes) {
+            if (h_sym_) (void)hipHostFree(h_sym_);
+            h_sym_ = nullptr;
+            h_sym_cap_ = 0;
+            if (hipHostMalloc(&h_sym_, bytes, hipHostMallocDefault) != hipSuccess) return 3;
+            h_sym_cap_ = bytes;
+        }
+        auto t0 = clk::now();
+        if (hipMemcpyAsync(h_sym_, d, bytes, hipMemcpyDeviceToHost, stream_) != hipSuccess) return 3;
+        if (hipStreamSynchronize(stream_) != hipSuccess) return 3;
+        if (st) st->d2h_ms += ms_since(t0);
+        *sym = (const uint8_t*)h_sym_;
+        return 0;
+    };
+
+    // data without a 16-bit sample: no predictor stage (the reference would
+    // reinterpret the buffer as uint16, klb_imageIO.cpp:2365)
+    const bool predictable = (bpp == 2) && h.Nnum > 0;
+    if (!predictable || (!autosel && k == 0)) {
+        if (!autosel && k > 7) return kErrBadPredictor;
+        h.headerVersion = (uint8_t)(hv & 0x80);
+        if (!dev) {
+            *sym = (const uint8_t*)img;
+            return 0;
+        }
+        if (int rc = ensure_gpu()) return rc;
+        return host_symbols_from_device(img, total_bytes);
+    }
+    if (!autosel && k > 7) {
+        std::printf("ERROR: predictor request %d is not valid (use 0-7 for auto, 8-15 for predictor 0-7)\n", req);
+        return kErrBadPredictor;
+    }
+    if (int rc = ensure_gpu()) return rc;
+    (void)hipSetDevice(device_);
+    const int fam = current_family();
+    const int T = h.Nnum;
+
+    const uint16_t* d_img = (const uint16_t*)img;
+    if (!dev && !dev_alloc(d_in_, d_in_cap_, vol * 2)) return 3;
+    if (!dev_alloc(d_sym_, d_sym_cap_, (dev ? V * vol : vol) * 2)) return 3;
+    if (!h_sym_ || h_sym_cap_ < total_bytes) {
+        if (h_sym_) (void)hipHostFree(h_sym_);
+        h_sym_ = nullptr;
+        h_sym_cap_ = 0;
+        if (hipHostMalloc(&h_sym_, total_bytes, hipHostMallocDefault) != hipSuccess) return 3;
+        h_sym_cap_ = total_bytes;
+    }
+    float pred_ms_total = 0.f;
+    for (uint64_t v = 0; v < V; ++v) {
+        const uint16_t* src;
+        if (dev) {
+            src = d_img + v * vol;
+        } else {
+            auto t0 = clk::now();
+            if (hipMemcpyAsync(d_in_, (const uint16_t*)img + v * vol, vol * 2, hipMemcpyHostToDevice, stream_) !=
+                hipSuccess)
+                return 3;
+            if (hipStreamSynchronize(stream_) != hipSuccess) return 3;
+            if (st) st->h2d_ms += ms_since(t0);
+            src = (const uint16_t*)d_in_;
+        }
+        if (v == 0 && autosel) {
+            // selection on frame 0 of volume (c=0, t=0) (klb_imageIO.cpp:2316-2360)
+            auto t0 = clk::now();
+            const size_t need = lfm_hip_select_workspace_bytes((int)W, (int)H);
+            if (!dev_alloc(d_ws_, d_ws_cap_, need)) return 3;
+            float ent[8];
+            int chosen = 0;
+            int rc = lfm_hip_select(src, (int)W, (int)H, T, fam, ent, &chosen, d_ws_, stream_);
+            if (rc != LFM_HIP_OK) return 3;
+            k = chosen;
+            if (st) {
+                st->select_ms += ms_since(t0);
+                std::memcpy(st->entropy, ent, sizeof(ent));
+            }
+        }
+        uint16_t* dst = (uint16_t*)d_sym_ + (dev ? v * vol : 0);
+        (void)hipEventRecord(ev0_, stream_);
+        int rc = lfm_hip_predict(src, nullptr, dst, (int)W, (int)H, (int)Z, T, fam, k, video, 0, stream_);
+        (void)hipEventRecord(ev1_, stream_);
+        if (rc != LFM_HIP_OK) return 3;
+        if (!dev) {
+            auto t0 = clk::now();
+            if (hipMemcpyAsync((uint8_t*)h_sym_ + v * vol * 2, dst, vol * 2, hipMemcpyDeviceToHost, stream_) !=
+                hipSuccess)
+                return 3;
+            if (hipStreamSynchronize(stream_) != hipSuccess) return 3;
+            if (st) st->d2h_ms += ms_since(t0);
+        } else if (hipEventSynchronize(ev1_) != hipSuccess) {
+            return 3;
+        }
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ev0_, ev1_);
+        pred_ms_total += ms;
+    }
+    if (dev) {
+        auto t0 = clk::now();
+        if (hipMemcpyAsync(h_sym_, d_sym_, total_bytes, hipMemcpyDeviceToHost, stream_) != hipSuccess) return 3;
+        if (hipStreamSynchronize(stream_) != hipSuccess) return 3;
+        if (st) st->d2h_ms += ms_since(t0);
+    }
+    if (st) st->predict_ms += pred_ms_total;
+    h.headerVersion = (uint8_t)((hv & 0x80) | k);
+    if (st) st->chosen = k;
+    *sym = (const uint8_t*)h_sym_;
+    return 0;
+}
+
+int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads)
+{
+    if (threads <= 0) threads = default_threads();
+    auto t0 = clk::now();
+    if (st) std::memset(st, 0, sizeof(*st));
+    if (h.getBytesPerPixel() == 0) return 5;
+    for (int d = 0; d < KLB_DATA_DIMS; ++d) {
+        if (h.xyzct[d] == 0) return 3;
+        if (h.blockSize[d] == 0) h.blockSize[d] = 1;
+        h.blockSize[d] = std::min(h.blockSize[d], h.xyzct[d]);  // klb_imageIO.cpp:2402-2404
+    }
+    if (h.compressionType != NONE && h.compressionType != BZIP2 && h.compressionType != ZLIB) {
+        std::printf("ERROR: compression type %d not implemented\n", (int)h.compressionType);
+        return 5;
+    }
+    const uint8_t* sym = nullptr;
+    int rc = predictor_stage(img, dev, h, &sym, st);
+    if (rc) return rc;
+    auto tc = clk::now();
+    rc = compress_blocks(sym, h, sink, threads);
+    if (st) {
+        st->compress_ms = ms_since(tc);
+        st->total_ms = ms_since(t0);
+        st->header_version = h.headerVersion;
+        st->chosen = h.headerVersion & 0x7F;
+        st->out_bytes = h.getCompressedFileSizeInBytes();
+    }
+    return rc;
+}
+
+Encoder& shared_encoder(std::unique_lock<std::mutex>& lock)
+{
+    static std::mutex mu;
+    static std::unique_ptr<Encoder> enc[64];
+    lock = std::unique_lock<std::mutex>(mu);
+    int dev = 0;
+    if (lfm_hip_device_count() > 0) {
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    dev = std::max(0, std::min(dev, 63));
+    if (!enc[dev]) enc[dev].reset(new Encoder(dev));
+    return *enc[dev];
+}
+
+// ---------------------------------------------------------------- decode --
+namespace {
+struct HostNb {
+    const uint16_t* f;
+    int W, T, x, y;
+    template <int N>
+    int at() const
+    {
+        int dx = 0, dy = 0;
+        if constexpr (N == NB_A) { dx = -1; }
+        if constexpr (N == NB_B) { dy = -1; }
+        if constexpr (N == NB_C) { dx = -1; dy = -1; }
+        if constexpr (N == NB_AP) { dx = -T; }
+        if constexpr (N == NB_BP) { dy = -T; }
+        if constexpr (N == NB_CP) { dx = -T; dy = -T; }
+        if constexpr (N == NB_AP1) { dx = -T - 1; }
+        if constexpr (N == NB_BP1) { dy = -T - 1; }
+        if constexpr (N == NB_ABP) { dx = -1; dy = -T; }
+        if constexpr (N == NB_BAP) { dx = -T; dy = -1; }
+        return (int)f[(size_t)(y + dy) * W + (x + dx)];
+    }
+};
+
+// prediction (spatial) or temporal prediction of the tiles family for a case
+template <int FAM, int K, int TC, int UC, bool TEMP>
+inline int inv_case(HostNb& g, int r, int P)
+{
+    constexpr int F = case_formula(FAM, K, TC, UC);
+    const int pr = eval_formula<F>(g);
+    if constexpr (!TEMP) return r + pr;
+    else if constexpr (F == F_Z) return r + P;
+    else return r + ((pr + P) >> 1);  // tiles: I = r + ((pred + P) >> 1)
+}
+
+template <int FAM, int K, bool TEMP>
+void unpredict_frame(const uint16_t* sym, const uint16_t* prev, uint16_t* out, int W, int H, int T)
+{
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            HostNb g{out, W, T, x, y};
+            const int tx = x / T, ty = y / T, u = x % T, v = y % T;
+            const int tc = tx == 0 ? (ty == 0 ? 0 : 1) : (ty == 0 ? 2 : 3);
+            const int uc = u == 0 ? (v > 0 ? 0 : 1) : (v == 0 ? 2 : 3);
+            const int r = unsymbolize16(sym[(size_t)y * W + x]);
+            const int P = TEMP ? (int)prev[(size_t)y * W + x] : 0;
+            int val = 0;
+            switch (tc * 4 + uc) {
+#define LFM_INV(TC_, UC_) case TC_ * 4 + UC_: val = inv_case<FAM, K, TC_, UC_, TEMP>(g, r, P); break;
+            LFM_INV(0, 0) LFM_INV(0, 1) LFM_INV(0, 2) LFM_INV(0, 3)
+            LFM_INV(1, 0) LFM_INV(1, 1) LFM_INV(1, 2) LFM_INV(1, 3)
+            LFM_INV(2, 0) LFM_INV(2, 1) LFM_INV(2, 2) LFM_INV(2, 3)
+            LFM_INV(3, 0) LFM_INV(3, 1) LFM_INV(3, 2) LFM_INV(3, 3)
+#undef LFM_INV
+            }
+            out[(size_t)y * W + x] = (uint16_t)val;
+        }
+}
+
+template <int FAM>
+int unpredict_dispatch_k(int k, bool temp, const uint16_t* sym, const uint16_t* prev, uint16_t* out, int W, int H,
+                         int T)
+{
+#define LFM_K(K_)                                                                          \
+    case K_:                                                                               \
+        if (temp) unpredict_frame<FAM, K_, true>(sym, prev, out, W, H, T);                 \
+        else unpredict_frame<FAM, K_, false>(sym, prev, out, W, H, T);                     \
+        return 0;
+    switch (k) { LFM_K(1) LFM_K(2) LFM_K(3) LFM_K(4) LFM_K(5) LFM_K(6) LFM_K(7) }
+#undef LFM_K
+    return 3;
+}
+
+int unpredict_one(int fam, int k, bool temp, const uint16_t* sym, const uint16_t* prev, uint16_t* out, int W, int H,
+                  int T)
+{
+    if (temp && fam != 0) return LFM_HIP_ENOTINV;  // r = ((I - pred) + P) >> 1 drops a bit
+    switch (fam) {
+    case 0: return unpredict_dispatch_k<0>(k, temp, sym, prev, out, W, H, T);
+    case 1: return unpredict_dispatch_k<1>(k, temp, sym, prev, out, W, H, T);
+    case 2: return unpredict_dispatch_k<2>(k, temp, sym, prev, out, W, H, T);
+    }
+    return 3;
+}
+
+template <class F>
+void parallel_for(uint64_t n, int threads, F&& f)
+{
+    std::atomic<uint64_t> next{0};
+    auto w = [&]() {
+        for (;;) {
+            uint64_t i = next.fetch_add(1);
+            if (i >= n) break;
+            f(i);
+        }
+    };
+    threads = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(threads, 1), n));
+    std::vector<std::thread> pool;
+    for (int i = 1; i < threads; ++i) pool.emplace_back(w);
+    w();
+    for (auto& t : pool) t.join();
+}
+} // namespace
+
+int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int threads,
+                   int family)
+{
+    if (threads <= 0) threads = default_threads();
+    const BlockGrid g(h);
+    if (g.nblocks != h.Nb) return 3;
+    const size_t bpp = h.getBytesPerPixel();
+    if (!bpp) return 5;
+    const int k = h.headerVersion & 0x7F;
+    const int video = (h.headerVersion >> 7) & 1;
+    const bool predicted = bpp == 2 && k != 0;
+    if (predicted && (k > 7 || h.Nnum == 0)) {
+        std::printf("ERROR: unknown predictor %d in header\n", k);
+        return 3;
+    }
+    std::vector<uint16_t> symbuf;
+    uint8_t* sym = img;
+    if (predicted) {
+        symbuf.resize(h.getImageSizePixels());
+        sym = (uint8_t*)symbuf.data();
+    }
+    std::atomic<int> err{0};
+    const uint32_t block_bytes = h.getBlockSizeBytes();
+    parallel_for(g.nblocks, threads, [&](uint64_t id) {
+        thread_local std::vector<uint8_t> scratch;
+        uint64_t o[5], s[5];
+        g.block(id, o, s);
+        const uint64_t expect = bpp * s[0] * s[1] * s[2] * s[3] * s[4];
+        const uint64_t off = h.getBlockOffset(id), n = h.getBlockCompressedSizeBytes(id);
+        if (off + n > len) { err.store(3); return; }
+        scratch.resize(std::max<uint64_t>(expect, block_bytes));
+        int rc = decompress_one(h.compressionType, payload + off, (uint32_t)n, scratch.data(), (uint32_t)expect);
+        if (rc) { err.store(rc); return; }
+        scatter_block(scratch.data(), g, id, bpp, sym);
+    });
+    if (err.load()) return err.load();
+    if (!predicted) return 0;
+    // inverse predictor (host, frames in parallel; on video stacks the odd
+    // frames need the decoded even frame before them)
+    const int W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
+    const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
+    const size_t fs = (size_t)W * H;
+    const uint16_t* s16 = symbuf.data();
+    uint16_t* o16 = (uint16_t*)img;
+    for (int pass = 0; pass < (video ? 2 : 1); ++pass) {
+        std::vector<uint64_t> frames;
+        for (uint64_t v = 0; v < V; ++v)
+            for (int z = 0; z < Z; ++z) {
+                const bool temp = video && (z & 1);
+                if (video ? (pass == (temp ? 1 : 0)) : true) frames.push_back(v * Z + z);
+            }
+        parallel_for(frames.size(), threads, [&](uint64_t i) {
+            const uint64_t fidx = frames[i];
+            const int z = (int)(fidx % Z);
+            const bool temp = video && (z & 1);
+            int rc = unpredict_one(family, k, temp, s16 + fidx * fs, temp ? o16 + (fidx - 1) * fs : nullptr,
+                                   o16 + fidx * fs, W, H, h.Nnum);
+            if (rc) err.store(rc == LFM_HIP_ENOTINV ? 3 : rc);
+        });
+        if (err.load()) {
+            std::printf("ERROR: frames of this file cannot be inverted (temporal angle/space predictor)\n");
+            return err.load();
+        }
+    }
+    return 0;
+}
+
+int decode_file(const char* filename, klb_image_header& h, std::vector<uint8_t>* img_out, uint8_t* img_into,
+                int threads)
+{
+    FILE* f = std::fopen(filename, "rb");
+    if (!f) {
+        std::printf("ERROR: file %s could not be opened\n", filename);
+        return 3;
+    }
+    std::fseek(f, 0, SEEK_END);
+    const long size = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    std::vector<uint8_t> buf(size > 0 ? (size_t)size : 0);
+    const size_t got = buf.empty() ? 0 : std::fread(buf.data(), 1, buf.size(), f);
+    std::fclose(f);
+    if (got != buf.size()) return 3;
+    int rc = h.parseHeader(buf.data(), buf.size());
+    if (rc) return rc;
+    uint8_t* dst = img_into;
+    if (!dst) {
+        img_out->resize(h.getImageSizeBytes());
+        dst = img_out->data();
+    }
+    const size_t hs = h.getSizeInBytes();
+    return decode_payload(buf.data() + hs, buf.size() - hs, h, dst, threads, current_family());
+}
+
+} // namespace lfm

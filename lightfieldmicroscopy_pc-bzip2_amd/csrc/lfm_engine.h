@@ -1,0 +1,100 @@
+// lfm_engine.h -- encode / decode engine behind klb_imageIO, the C ABI and
+// the lfm_encoder API.
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <mutex>
+#include <vector>
+#include <hip/hip_runtime.h>
+#include "klb_imageHeader.h"
+#include "lfm_api.h"
+
+namespace lfm {
+
+// error codes beyond the reference's 2 / 3 / 5
+constexpr int kErrBadPredictor = 6;
+constexpr int kErrNoGpu = 7;
+
+int default_threads();      // env LFM_NUM_THREADS, else OMP_NUM_THREADS, else hardware_concurrency
+int current_family();       // lfm_set_family / env LFM_PREDICTOR_WAY / LFM_PREDICTOR_WAY
+void set_family(int fam);
+
+// x-fastest decomposition of the 5-D image into blocks (klb_imageIO.cpp:98-160)
+struct BlockGrid {
+    uint64_t dims[5], bs[5], nb[5], stride[5], nblocks;
+    explicit BlockGrid(const klb_image_header& h);
+    void block(uint64_t id, uint64_t origin[5], uint64_t size[5]) const;
+};
+void gather_block(const uint8_t* img, const BlockGrid& g, uint64_t id, size_t bpp, uint8_t* dst, size_t* nbytes);
+void scatter_block(const uint8_t* blk, const BlockGrid& g, uint64_t id, size_t bpp, uint8_t* img);
+
+// output of an encode: a file (reference writer order: header, blocks, then
+// the offset table rewritten) or a memory buffer
+class Sink {
+public:
+    virtual ~Sink() = default;
+    virtual int begin(const klb_image_header& h) = 0;
+    virtual int append(const uint8_t* p, size_t n) = 0;
+    virtual int finish(const klb_image_header& h) = 0;
+};
+class FileSink : public Sink {
+public:
+    explicit FileSink(FILE* f) : f_(f) {}
+    int begin(const klb_image_header& h) override;
+    int append(const uint8_t* p, size_t n) override;
+    int finish(const klb_image_header& h) override;
+private:
+    FILE* f_;
+    std::vector<char> vbuf_;
+};
+class MemSink : public Sink {
+public:
+    explicit MemSink(std::vector<uint8_t>* out) : out_(out) {}
+    int begin(const klb_image_header& h) override;
+    int append(const uint8_t* p, size_t n) override;
+    int finish(const klb_image_header& h) override;
+private:
+    std::vector<uint8_t>* out_;
+};
+
+// Compress every block of `sym` (image layout, bpp bytes per pixel) in
+// parallel and hand them to the sink in block order.  `h` must already hold
+// the clamped block size; its blockOffset table is filled.
+int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads);
+
+// Encoder: GPU predictor stage + block compression.  One per device; keeps
+// device / pinned buffers between calls.
+class Encoder {
+public:
+    explicit Encoder(int device);
+    ~Encoder();
+    // img: host pointer (dev=false) or device pointer on this encoder's device
+    int encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads);
+    std::vector<uint8_t> mem_out;
+    int device() const { return device_; }
+
+private:
+    int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, lfm_encode_stats* st);
+    int ensure_gpu();
+    void* dev_alloc(void*& p, size_t& cap, size_t need);
+    int device_;
+    bool gpu_ready_ = false;
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    void* d_in_ = nullptr;  size_t d_in_cap_ = 0;
+    void* d_sym_ = nullptr; size_t d_sym_cap_ = 0;
+    void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
+    void* h_sym_ = nullptr; size_t h_sym_cap_ = 0;   // pinned
+};
+
+// process-wide encoder for the C ABI / klb_imageIO (serialised by its mutex)
+Encoder& shared_encoder(std::unique_lock<std::mutex>& lock);
+
+// Decode the payload of a .lfm (bytes after the header) into img.
+int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int threads,
+                   int family);
+int decode_file(const char* filename, klb_image_header& h, std::vector<uint8_t>* img_out, uint8_t* img_into,
+                int threads);
+
+} // namespace lfm

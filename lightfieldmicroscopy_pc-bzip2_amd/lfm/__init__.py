@@ -1,0 +1,305 @@
+"""ctypes binding of liblfm.so (the MI355X-native .lfm encoder / decoder).
+
+This is the same C ABI a Matlab MEX, a JNI wrapper or any other FFI caller
+binds (include/lfm/*.h); Python is only a test / bench harness here.
+
+GPU entry points need a visible gfx950 device; they raise LfmError when the
+library or the device is missing (there is no CPU fallback for the predictor
+stage).  When PyTorch is importable it is imported BEFORE liblfm.so is loaded,
+so both share one HIP runtime (libamdhip64.so.7) in the process.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+try:  # one HIP runtime per process: torch's, if torch is present
+    import torch  # noqa: F401
+    _HAVE_TORCH = True
+except Exception:  # pragma: no cover
+    _HAVE_TORCH = False
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "liblfm.so")
+
+FAMILIES = {"tiles": 0, "angle_and_space": 0, "angle": 1, "space": 2}
+DTYPES = {np.dtype(np.uint8): 0, np.dtype(np.uint16): 1, np.dtype(np.uint32): 2, np.dtype(np.uint64): 3,
+          np.dtype(np.int8): 4, np.dtype(np.int16): 5, np.dtype(np.int32): 6, np.dtype(np.int64): 7,
+          np.dtype(np.float32): 8, np.dtype(np.float64): 9}
+NP_OF = {v: k for k, v in DTYPES.items()}
+
+EXPORTS = [
+    # klb_Cwrapper.h
+    "writeKLBstack", "writeKLBstackSlices", "readKLBheader", "readKLBstack", "readKLBstackInPlace",
+    "readKLBroiInPlace",
+    # lfm_api.h
+    "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
+    "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_decode_memory",
+    # lfm_hip.h
+    "lfm_hip_predict", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
+    "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic",
+]
+
+
+class LfmError(RuntimeError):
+    pass
+
+
+class EncodeStats(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
+                ("predict_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double), ("compress_ms", ctypes.c_double),
+                ("chosen", ctypes.c_int), ("header_version", ctypes.c_int), ("entropy", ctypes.c_float * 8),
+                ("out_bytes", ctypes.c_uint64)]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "entropy"}
+        d["entropy"] = list(self.entropy)
+        return d
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LfmError("liblfm.so is not built (run `make -C %s` or __graft_entry__.build())" % PKG_DIR)
+    L = ctypes.CDLL(LIB_PATH)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    f32p = ctypes.POINTER(ctypes.c_float)
+    vp = ctypes.c_void_p
+    L.writeKLBstack.argtypes = [vp, ctypes.c_char_p, u32p, ctypes.c_int, ctypes.c_int, f32p, u32p, ctypes.c_int,
+                                ctypes.c_char_p]
+    L.writeKLBstackSlices.argtypes = [ctypes.POINTER(vp), ctypes.c_char_p, u32p, ctypes.c_int, ctypes.c_int, f32p,
+                                      u32p, ctypes.c_int, ctypes.c_char_p]
+    L.readKLBheader.argtypes = [ctypes.c_char_p, u32p, ctypes.POINTER(ctypes.c_int), f32p, u32p,
+                                ctypes.POINTER(ctypes.c_int), ctypes.c_char_p]
+    L.readKLBstack.restype = vp
+    L.readKLBstack.argtypes = [ctypes.c_char_p, u32p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, f32p, u32p,
+                               ctypes.POINTER(ctypes.c_int), ctypes.c_char_p]
+    L.readKLBstackInPlace.argtypes = [ctypes.c_char_p, vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.readKLBroiInPlace.argtypes = [ctypes.c_char_p, vp, u32p, u32p, ctypes.c_int]
+    L.lfm_version.restype = ctypes.c_char_p
+    L.writeLFMstack_c.argtypes = [vp, ctypes.c_char_p, u32p, ctypes.c_int, ctypes.c_int, f32p, u32p, ctypes.c_int,
+                                  ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.readLFMstack_c.argtypes = [ctypes.c_char_p, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8),
+                                 ctypes.POINTER(ctypes.c_uint8)]
+    L.lfm_encoder_create.restype = vp
+    L.lfm_encoder_create.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.lfm_encoder_destroy.argtypes = [vp]
+    L.lfm_encoder_encode.argtypes = [vp, vp, ctypes.c_int, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p,
+                                     ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
+    L.lfm_decode_memory.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_int]
+    L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
+    L.lfm_hip_entropy2d.argtypes = [vp, ctypes.c_uint64, f32p, vp]
+    L.lfm_hip_select_workspace_bytes.restype = ctypes.c_size_t
+    L.lfm_hip_select_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.lfm_hip_select.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p,
+                                 ctypes.POINTER(ctypes.c_int), vp, vp]
+    L.lfm_hip_synth.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_uint64, ctypes.c_uint64, vp]
+    _lib = L
+    return L
+
+
+def missing_exports():
+    L = lib()
+    return [name for name in EXPORTS if not hasattr(L, name)]
+
+
+def device_count():
+    return int(lib().lfm_hip_device_count())
+
+
+def require_gpu():
+    if device_count() <= 0:
+        raise LfmError("no HIP device visible: the LFM predictor stage runs only on the GPU")
+
+
+def set_family(family):
+    if lib().lfm_set_family(FAMILIES.get(family, family)) != 0:
+        raise LfmError("bad family %r" % (family,))
+
+
+def get_family():
+    return int(lib().lfm_get_family())
+
+
+def _u32(v):
+    return (ctypes.c_uint32 * 5)(*[int(x) for x in v])
+
+
+def _f32(v):
+    return (ctypes.c_float * 5)(*[float(x) for x in v])
+
+
+def _xyzct(arr):
+    a = arr
+    while a.ndim < 5:
+        a = a[None]
+    t, c, z, y, x = a.shape
+    return [x, y, z, c, t]
+
+
+def _meta(m):
+    if m is None:
+        return None
+    b = m.encode() if isinstance(m, str) else bytes(m)
+    return ctypes.create_string_buffer(b[:256].ljust(256, b"\0"), 256)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise LfmError("%s failed with code %d" % (what, rc))
+
+
+# ------------------------------------------------------------- file API --
+def write_lfm(path, img, predictor_request=0, nnum=13, video=0, block_size=None, pixel_size=None,
+              compression=1, metadata=None, num_threads=-1, family=None):
+    """MEX writeLFMstack semantics.  img: ndarray indexed [t, c, z, y, x] (or fewer leading dims)."""
+    img = np.ascontiguousarray(img)
+    if family is not None:
+        set_family(family)
+    xyzct = _xyzct(img)
+    rc = lib().writeLFMstack_c(img.ctypes.data, os.fsencode(path), _u32(xyzct), DTYPES[img.dtype], num_threads,
+                               _f32(pixel_size) if pixel_size is not None else None,
+                               _u32(block_size) if block_size is not None else None, compression, _meta(metadata),
+                               int(predictor_request), int(nnum), int(video))
+    _check(rc, "writeLFMstack_c")
+
+
+def write_klb(path, img, block_size=None, pixel_size=None, compression=1, metadata=None, num_threads=-1):
+    """writeKLBstack (C ABI): headerVersion 0 (auto predictor), Nnum 13."""
+    img = np.ascontiguousarray(img)
+    rc = lib().writeKLBstack(img.ctypes.data, os.fsencode(path), _u32(_xyzct(img)), DTYPES[img.dtype], num_threads,
+                             _f32(pixel_size) if pixel_size is not None else None,
+                             _u32(block_size) if block_size is not None else None, compression, _meta(metadata))
+    _check(rc, "writeKLBstack")
+
+
+def read_header(path):
+    xyzct = (ctypes.c_uint32 * 5)()
+    dt = ctypes.c_int()
+    ps = (ctypes.c_float * 5)()
+    bs = (ctypes.c_uint32 * 5)()
+    ct = ctypes.c_int()
+    md = ctypes.create_string_buffer(256)
+    _check(lib().readKLBheader(os.fsencode(path), xyzct, ctypes.byref(dt), ps, bs, ctypes.byref(ct), md),
+           "readKLBheader")
+    return dict(xyzct=list(xyzct), data_type=dt.value, pixel_size=list(ps), block_size=list(bs),
+                compression=ct.value, metadata=md.raw)
+
+
+def read_lfm(path, num_threads=-1, family=None):
+    """Decode a .lfm file; returns (ndarray [t, c, z, y, x], header_version, nnum)."""
+    if family is not None:
+        set_family(family)
+    h = read_header(path)
+    x, y, z, c, t = h["xyzct"]
+    out = np.empty((t, c, z, y, x), dtype=NP_OF[h["data_type"]])
+    hv = ctypes.c_uint8()
+    nn = ctypes.c_uint8()
+    _check(lib().readLFMstack_c(os.fsencode(path), out.ctypes.data, num_threads, ctypes.byref(hv), ctypes.byref(nn)),
+           "readLFMstack_c")
+    return out, hv.value, nn.value
+
+
+# ------------------------------------------------------ in-memory encoder --
+class Encoder:
+    """lfm_encoder: encode host arrays or device-resident tensors to .lfm bytes."""
+
+    def __init__(self, device=-1, num_threads=-1):
+        self._h = lib().lfm_encoder_create(device, num_threads)
+        if not self._h:
+            raise LfmError("lfm_encoder_create failed")
+
+    def close(self):
+        if self._h:
+            lib().lfm_encoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode(self, img, header_version=0, nnum=13, block_size=None, compression=1, metadata=None,
+               xyzct=None, data_type=None):
+        """img: numpy array [t,c,z,y,x] (host) or a torch CUDA tensor (device, uint16 viewed as int16 ok).
+        Returns (bytes_view, stats dict)."""
+        dev = 0
+        if _HAVE_TORCH and isinstance(img, torch.Tensor):
+            if not img.is_cuda:
+                img = img.numpy()
+            else:
+                dev = 1
+                ptr = img.data_ptr()
+                shape = list(img.shape)
+                while len(shape) < 5:
+                    shape = [1] + shape
+                xyzct = xyzct or [shape[4], shape[3], shape[2], shape[1], shape[0]]
+                data_type = 1 if data_type is None else data_type
+        if not dev:
+            img = np.ascontiguousarray(img)
+            ptr = img.ctypes.data
+            xyzct = xyzct or _xyzct(img)
+            data_type = DTYPES[img.dtype] if data_type is None else data_type
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_uint64()
+        st = EncodeStats()
+        rc = lib().lfm_encoder_encode(self._h, ptr, dev, _u32(xyzct), data_type, int(header_version), int(nnum),
+                                      _u32(block_size) if block_size is not None else None, compression,
+                                      _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
+        _check(rc, "lfm_encoder_encode")
+        buf = ctypes.string_at(out, n.value)
+        return buf, st.as_dict()
+
+
+def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):
+    if shape_tczyx is None:
+        import struct
+        xyzct = struct.unpack_from("<5I", buf, 2)
+        dtype = NP_OF[buf[42]]
+        shape_tczyx = (xyzct[4], xyzct[3], xyzct[2], xyzct[1], xyzct[0])
+    out = np.empty(shape_tczyx, dtype=dtype)
+    _check(lib().lfm_decode_memory(buf, len(buf), out.ctypes.data, num_threads), "lfm_decode_memory")
+    return out
+
+
+# ------------------------------------------------------ device primitives --
+def _stream(stream):
+    if stream is None:
+        return None
+    return ctypes.c_void_p(int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream))
+
+
+def predict_device(d_in, d_out, W, H, nframes, T, family, predictor, video=0, z0=0, d_prev=None, stream=None):
+    """Launch the fused predictor + symbolize kernel on device tensors (or raw pointers)."""
+    p = lambda t: None if t is None else (t.data_ptr() if hasattr(t, "data_ptr") else int(t))  # noqa: E731
+    rc = lib().lfm_hip_predict(p(d_in), p(d_prev), p(d_out), W, H, nframes, T, FAMILIES.get(family, family),
+                               predictor, video, z0, _stream(stream))
+    _check(rc, "lfm_hip_predict")
+
+
+def select_device(d_frame, W, H, T, family, stream=None):
+    ent = (ctypes.c_float * 8)()
+    k = ctypes.c_int()
+    rc = lib().lfm_hip_select(d_frame.data_ptr(), W, H, T, FAMILIES.get(family, family), ent, ctypes.byref(k), None,
+                              _stream(stream))
+    _check(rc, "lfm_hip_select")
+    return k.value, np.array(list(ent), dtype=np.float32)
+
+
+def entropy_device(d_cand, npix=None, stream=None):
+    e = ctypes.c_float()
+    n = d_cand.numel() if npix is None else npix
+    _check(lib().lfm_hip_entropy2d(d_cand.data_ptr(), n, ctypes.byref(e), _stream(stream)), "lfm_hip_entropy2d")
+    return e.value
+
+
+def synth_device(d_out, X, Y, Z, T, t_index=0, idx0=0, seed=0x4C464D00, stream=None):
+    _check(lib().lfm_hip_synth(d_out.data_ptr(), X, Y, Z, T, t_index, idx0, seed, _stream(stream)), "lfm_hip_synth")

@@ -1,0 +1,433 @@
+/*
+ * lfm_oracle.c -- CPU restatement of the reference LFM predictor path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (liblfm.so, the HIP
+ * kernels, the host encoder) links, loads or calls this file.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, and only as
+ * the checker / the timed CPU baseline.
+ *
+ * Parity status (see DESIGN.md "Oracle"):
+ *   - predictor residual arithmetic: restated case by case from the reference
+ *     kernels' source text; the reference kernels cannot be built here (they
+ *     need nvcc, cuda_runtime.h and thrust), so this part is PARITY UNPINNED by
+ *     execution.  oracle/audit_tables.py compares every case of the tables
+ *     below with the reference's assignment expressions as text (it executes
+ *     nothing from the reference).  Round trips through the inverse below pin
+ *     self-consistency (the reference's own test strategy,
+ *     test/mainTest_lfmIO.cxx:129-140, matlabWrapper/test.m:16-19).
+ *   - 2D entropy: restated from klb_imageIO.cpp:2030-2093 and
+ *     lfm_Predictors.cu:2833-2949; float summation order is unpinned in the
+ *     reference (thrust::reduce), so entropies are compared with a tolerance.
+ *
+ * Notation: frame W x H, x fastest; T = Nnum;
+ * tx = x / T, ty = y / T, u = x % T, v = y % T;
+ * A = I(x-1,y)  B = I(x,y-1)  C = I(x-1,y-1)
+ * Ap = I(x-T,y) Bp = I(x,y-T) Cp = I(x-T,y-T)
+ * Ap1 = I(x-T-1,y)  Bp1 = I(x,y-T-1)  ABp = I(x-1,y-T)  BAp = I(x-T,y-1)
+ * P = previous (raw) frame at (x,y).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+/* ---------------------------------------------------------------------------
+ * Spatial prediction formulas.  Every formula is written with the same
+ * operand order and parenthesisation as the reference expression it restates
+ * (audit_tables.py parses the `case F_xxx: return ...;` lines below).
+ * ------------------------------------------------------------------------- */
+enum {
+    F_Z = 0,      /* pred 0: residual = I                                   */
+    F_A, F_B, F_C, F_AP, F_BP, F_CP,
+    F_AVG_A_AP, F_AVG_B_BP, F_AVG_A_BP, F_AVG_C_BP, F_AVG_B_AP,
+    F_AVG_C_AP, F_AVG_B_CP, F_AVG_A_CP, F_AVG_C_CP, F_AVG_A_B, F_AVG_B_A,
+    F_AVG_BP_AP,
+    F_ABC, F_BAC, F_ABC_SUM,                  /* A+B-C (two spellings) */
+    F_P4_0Y, F_P4_X0, F_P4_COL, F_P4_CORNER, F_P4_ROW, F_P4_IN,
+    F_P5_00Q,                                 /* (A+(B-C))>>1 precedence quirk */
+    F_P5_0Y, F_P5_X0, F_P5_COL, F_P5_CORNER, F_P5_ROW, F_P5_IN,
+    F_A_HBC, F_B_HAC,                         /* A+((B-C)>>1), B+((A-C)>>1) */
+    F_P6_0Y, F_P6_X0, F_P6_COL, F_P6_CORNER, F_P6_ROW, F_P6_IN,
+    F_P7_0Y, F_P7_X0, F_P7_IN,
+    F_NUM
+};
+
+typedef struct {
+    const uint16_t* img;  /* current frame */
+    int W, T, x, y;
+} nbr_t;
+
+static inline int px(const nbr_t* n, int dx, int dy)
+{
+    int xx = n->x + dx, yy = n->y + dy;
+    if (xx < 0 || yy < 0) abort(); /* never happens: every case only reaches up/left inside the frame */
+    return (int)n->img[(size_t)yy * n->W + xx];
+}
+
+static int pred_formula(int f, const nbr_t* n)
+{
+    const int T = n->T;
+#define A   px(n, -1, 0)
+#define B   px(n, 0, -1)
+#define C   px(n, -1, -1)
+#define Ap  px(n, -T, 0)
+#define Bp  px(n, 0, -T)
+#define Cp  px(n, -T, -T)
+#define Ap1 px(n, -T - 1, 0)
+#define Bp1 px(n, 0, -T - 1)
+#define ABp px(n, -1, -T)
+#define BAp px(n, -T, -1)
+    switch (f) {
+    case F_Z: return 0;
+    case F_A: return A;
+    case F_B: return B;
+    case F_C: return C;
+    case F_AP: return Ap;
+    case F_BP: return Bp;
+    case F_CP: return Cp;
+    case F_AVG_A_AP: return (A + Ap) >> 1;
+    case F_AVG_B_BP: return (B + Bp) >> 1;
+    case F_AVG_A_BP: return (A + Bp) >> 1;
+    case F_AVG_C_BP: return (C + Bp) >> 1;
+    case F_AVG_B_AP: return (B + Ap) >> 1;
+    case F_AVG_C_AP: return (C + Ap) >> 1;
+    case F_AVG_B_CP: return (B + Cp) >> 1;
+    case F_AVG_A_CP: return (A + Cp) >> 1;
+    case F_AVG_C_CP: return (C + Cp) >> 1;
+    case F_AVG_A_B: return (A + B) >> 1;
+    case F_AVG_B_A: return (B + A) >> 1;
+    case F_AVG_BP_AP: return (Bp + Ap) >> 1;
+    case F_ABC: return A + B - C;
+    case F_BAC: return B + A - C;
+    case F_ABC_SUM: return Bp + Ap - Cp;
+    case F_P4_0Y: return (A + B - C + Bp) >> 1;
+    case F_P4_X0: return (A + B - C + Ap) >> 1;
+    case F_P4_COL: return (Bp + Ap - Cp + B) >> 1;
+    case F_P4_CORNER: return Bp + Ap - Cp;
+    case F_P4_ROW: return (Bp + Ap - Cp + A) >> 1;
+    case F_P4_IN: return (Bp + Ap - Cp + B + A - C) >> 1;
+    case F_P5_00Q: return (A + (B - C)) >> 1;
+    case F_P5_0Y: return (A + ((B - C) >> 1) + Bp) >> 1;
+    case F_P5_X0: return (A + ((B - C) >> 1) + Ap) >> 1;
+    case F_P5_COL: return (Bp + ((Ap - Cp) >> 1) + B) >> 1;
+    case F_P5_CORNER: return Bp + ((Ap - Cp) >> 1);
+    case F_P5_ROW: return (Bp + ((Ap - Cp) >> 1) + A) >> 1;
+    case F_P5_IN: return (Bp + ((Ap - Cp) >> 1) + B + ((A - C) >> 1)) >> 1;
+    case F_A_HBC: return A + ((B - C) >> 1);
+    case F_B_HAC: return B + ((A - C) >> 1);
+    case F_P6_0Y: return (B + ((A - C) >> 1) + Bp) >> 1;
+    case F_P6_X0: return (B + ((A - C) >> 1) + Ap) >> 1;
+    case F_P6_COL: return (Ap + ((Bp - Cp) >> 1) + B) >> 1;
+    case F_P6_CORNER: return Ap + ((Bp - Cp) >> 1);
+    case F_P6_ROW: return (Ap + ((Bp - Cp) >> 1) + A) >> 1;
+    case F_P6_IN: return (Ap + ((Bp - Cp) >> 1) + A + ((B - C) >> 1)) >> 1;
+    case F_P7_0Y: return (A + B + ABp + Bp1) >> 2;
+    case F_P7_X0: return (A + B + BAp + Ap1) >> 2;
+    case F_P7_IN: return (Bp1 + Ap1 + B + A) >> 2;
+    default: abort();
+    }
+#undef A
+#undef B
+#undef C
+#undef Ap
+#undef Bp
+#undef Cp
+#undef Ap1
+#undef Bp1
+#undef ABp
+#undef BAp
+}
+
+/* Case indices: tile case tc = {tx==0&&ty==0, tx==0&&ty!=0, tx!=0&&ty==0, other};
+ * position case uc = {u==0&&v>0, u==0&&v==0, u>0&&v==0, u>0&&v>0}.
+ * This is the if/else structure every one of the 21 reference kernels uses
+ * (e.g. lfm_Predictors.cu:53-123 for tiles P1). */
+
+/* tiles family ("ANGLE_AND_SPACE", LFM_PREDICTOR_WAY 0): lfm_Predictors.cu */
+static const unsigned char TAB_TILES[7][4][4] = {
+    /* P1: _predictor1_tiles, line 35 */
+    {{F_B, F_Z, F_A, F_A}, {F_B, F_BP, F_A, F_A},
+     {F_AP, F_AP, F_AVG_A_AP, F_AVG_A_AP}, {F_AP, F_AP, F_AVG_A_AP, F_AVG_A_AP}},
+    /* P2: _predictor2_tiles, line 201 */
+    {{F_B, F_Z, F_A, F_B}, {F_AVG_B_BP, F_BP, F_BP, F_AVG_B_BP},
+     {F_B, F_AP, F_A, F_B}, {F_BP, F_BP, F_AVG_B_BP, F_AVG_B_BP}},
+    /* P3: _predictor3_tiles, line 367 */
+    {{F_B, F_Z, F_A, F_C}, {F_AVG_B_BP, F_BP, F_AVG_A_BP, F_AVG_C_BP},
+     {F_AVG_B_AP, F_AP, F_AVG_A_AP, F_AVG_C_AP}, {F_AVG_B_CP, F_CP, F_AVG_A_CP, F_AVG_C_CP}},
+    /* P4: _predictor4_tiles, line 533 */
+    {{F_B, F_Z, F_A, F_ABC}, {F_AVG_B_BP, F_BP, F_AVG_A_BP, F_P4_0Y},
+     {F_AVG_B_AP, F_AP, F_AVG_A_AP, F_P4_X0}, {F_P4_COL, F_P4_CORNER, F_P4_ROW, F_P4_IN}},
+    /* P5: _predictor5_tiles, line 710 (tile (0,0) interior keeps the (A+(B-C))>>1 precedence of :744) */
+    {{F_B, F_Z, F_A, F_P5_00Q}, {F_AVG_B_BP, F_BP, F_AVG_A_BP, F_P5_0Y},
+     {F_AVG_B_AP, F_AP, F_AVG_A_AP, F_P5_X0}, {F_P5_COL, F_P5_CORNER, F_P5_ROW, F_P5_IN}},
+    /* P6: _predictor6_tiles, line 887 */
+    {{F_B, F_Z, F_A, F_B_HAC}, {F_AVG_B_BP, F_BP, F_AVG_A_BP, F_P6_0Y},
+     {F_AVG_B_AP, F_AP, F_AVG_A_AP, F_P6_X0}, {F_P6_COL, F_P6_CORNER, F_P6_ROW, F_P6_IN}},
+    /* P7: _predictor7_tiles, line 1065 */
+    {{F_B, F_Z, F_A, F_AVG_A_B}, {F_AVG_B_BP, F_BP, F_AVG_A_BP, F_P7_0Y},
+     {F_AVG_B_AP, F_AP, F_AVG_A_AP, F_P7_X0}, {F_P4_COL, F_P4_CORNER, F_P4_ROW, F_P7_IN}},
+};
+
+/* angle family (LFM_PREDICTOR_WAY 1): lfm_Predictors_angle.cu */
+static const unsigned char TAB_ANGLE[7][4][4] = {
+    /* P1: _predictor1_angle, line 17 */
+    {{F_B, F_Z, F_A, F_A}, {F_B, F_BP, F_A, F_A}, {F_B, F_AP, F_A, F_A}, {F_B, F_AP, F_A, F_A}},
+    /* P2: _predictor2_angle, line 222 */
+    {{F_B, F_Z, F_A, F_B}, {F_B, F_BP, F_A, F_B}, {F_B, F_AP, F_A, F_B}, {F_B, F_BP, F_B, F_B}},
+    /* P3: _predictor3_angle, line 423 */
+    {{F_B, F_Z, F_A, F_C}, {F_B, F_BP, F_A, F_C}, {F_B, F_AP, F_A, F_C}, {F_B, F_CP, F_A, F_C}},
+    /* P4: _predictor4_angle, line 589 */
+    {{F_B, F_Z, F_A, F_ABC}, {F_B, F_BP, F_A, F_ABC}, {F_B, F_AP, F_A, F_ABC}, {F_B, F_ABC_SUM, F_A, F_BAC}},
+    /* P5: _predictor5_angle, line 761 */
+    {{F_B, F_Z, F_A, F_A_HBC}, {F_B, F_BP, F_A, F_A_HBC}, {F_B, F_AP, F_A, F_A_HBC}, {F_B, F_P5_CORNER, F_A, F_B_HAC}},
+    /* P6: _predictor6_angle, line 940 (tile-interior IN case is A+((B-C)>>1), swapped w.r.t. the border tiles) */
+    {{F_B, F_Z, F_A, F_B_HAC}, {F_B, F_BP, F_A, F_B_HAC}, {F_B, F_AP, F_A, F_B_HAC}, {F_B, F_P6_CORNER, F_A, F_A_HBC}},
+    /* P7: _predictor7_angle, line 1112 */
+    {{F_B, F_Z, F_A, F_AVG_A_B}, {F_B, F_BP, F_A, F_AVG_A_B}, {F_B, F_AP, F_A, F_AVG_A_B}, {F_B, F_ABC_SUM, F_A, F_AVG_B_A}},
+};
+
+/* space family (LFM_PREDICTOR_WAY 2): lfm_Predictors_space.cu */
+static const unsigned char TAB_SPACE[7][4][4] = {
+    /* P1: _predictor1_space, line 17 */
+    {{F_B, F_Z, F_A, F_A}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP}, {F_AP, F_AP, F_AP, F_AP}},
+    /* P2: _predictor2_space, line 186 */
+    {{F_B, F_Z, F_A, F_B}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP}, {F_BP, F_BP, F_BP, F_BP}},
+    /* P3: _predictor3_space, line 353 */
+    {{F_B, F_Z, F_A, F_C}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP}, {F_CP, F_CP, F_CP, F_CP}},
+    /* P4: _predictor4_space, line 519 */
+    {{F_B, F_Z, F_A, F_ABC}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP},
+     {F_ABC_SUM, F_ABC_SUM, F_ABC_SUM, F_ABC_SUM}},
+    /* P5: _predictor5_space, line 694 */
+    {{F_B, F_Z, F_A, F_A_HBC}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP},
+     {F_P5_CORNER, F_P5_CORNER, F_P5_CORNER, F_P5_CORNER}},
+    /* P6: _predictor6_space, line 868 */
+    {{F_B, F_Z, F_A, F_B_HAC}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP},
+     {F_P6_CORNER, F_P6_CORNER, F_P6_CORNER, F_P6_CORNER}},
+    /* P7: _predictor7_space, line 1041 */
+    {{F_B, F_Z, F_A, F_AVG_A_B}, {F_BP, F_BP, F_BP, F_BP}, {F_AP, F_AP, F_AP, F_AP},
+     {F_ABC_SUM, F_ABC_SUM, F_ABC_SUM, F_AVG_BP_AP}},
+};
+
+/* Temporal cases of the angle/space families where the reference applies the
+ * "+P >> 1" twice: angle P4 tile-interior corner/row (lfm_Predictors_angle.cu,
+ * second half of _predictor4_angle) and space P6 tile (0,0) row case
+ * (second half of _predictor6_space). */
+static int temporal_double(int fam, int k, int tc, int uc)
+{
+    if (fam == 1 && k == 4 && tc == 3 && (uc == 1 || uc == 2)) return 1;
+    if (fam == 2 && k == 6 && tc == 0 && uc == 2) return 1;
+    return 0;
+}
+
+static const unsigned char (*family_table(int fam))[4][4]
+{
+    switch (fam) {
+    case 0: return TAB_TILES;
+    case 1: return TAB_ANGLE;
+    case 2: return TAB_SPACE;
+    default: return NULL;
+    }
+}
+
+/* exported for audit_tables.py */
+int lfmo_case_formula(int fam, int k, int tc, int uc) { return family_table(fam)[k - 1][tc][uc]; }
+int lfmo_case_temporal_double(int fam, int k, int tc, int uc) { return temporal_double(fam, k, tc, uc); }
+
+static inline int tile_case(int tx, int ty)
+{
+    if (tx == 0 && ty == 0) return 0;
+    if (tx == 0) return 1;
+    if (ty == 0) return 2;
+    return 3;
+}
+static inline int pos_case(int u, int v)
+{
+    if (u == 0) return v > 0 ? 0 : 1;
+    return v == 0 ? 2 : 3;
+}
+
+/* Full-precision residual (int) of one pixel, before the int16 store.
+ * Spatial: r = I - pred.  Temporal (zflag):
+ *   tiles  r = I - ((pred + P) >> 1)          e.g. lfm_Predictors.cu:131-193
+ *   angle/space r = ((I - pred) + P) >> 1     e.g. lfm_Predictors_angle.cu:136-192
+ *   pred == 0 case (lens (0,0), pixel (0,0)): r = I - P in every family. */
+int lfmo_residual(const uint16_t* cur, const uint16_t* prev, int W, int H, int T,
+                  int fam, int k, int zflag, int x, int y)
+{
+    (void)H;
+    nbr_t n = {cur, W, T, x, y};
+    int tx = x / T, ty = y / T, u = x % T, v = y % T;
+    int tc = tile_case(tx, ty), uc = pos_case(u, v);
+    int f = family_table(fam)[k - 1][tc][uc];
+    int I = (int)cur[(size_t)y * W + x];
+    if (!zflag) {
+        return I - pred_formula(f, &n);
+    }
+    int P = (int)prev[(size_t)y * W + x];
+    if (f == F_Z) return I - P;
+    int pr = pred_formula(f, &n);
+    if (fam == 0) return I - ((pr + P) >> 1);
+    if (temporal_double(fam, k, tc, uc)) return ((((I - pr) + P) >> 1) + P) >> 1;
+    return ((I - pr) + P) >> 1;
+}
+
+/* symbolize: lfm_Predictors.cu:16-26 on the int16-stored residual */
+static inline uint16_t symbolize16(int16_t r)
+{
+    int v = (int)r;
+    return (uint16_t)(uint32_t)(2 * abs(v) + (v >> 31));
+}
+/* unsymbolize: lfm_Predictors.cu:28-33 */
+static inline int16_t unsymbolize16(uint16_t s)
+{
+    int neg = s % 2;
+    return (int16_t)((1 - 2 * neg) * (((int)s + neg) / 2));
+}
+
+uint16_t lfmo_symbolize(int16_t r) { return symbolize16(r); }
+int16_t lfmo_unsymbolize(uint16_t s) { return unsymbolize16(s); }
+
+/* One frame of Predictor_both / _angle / _space (klb_imageIO.cpp:1244-1313):
+ * k == 0 copies the raw frame, otherwise residual -> int16 -> symbolize. */
+void lfmo_predict_frame(const uint16_t* cur, const uint16_t* prev, uint16_t* out,
+                        int W, int H, int T, int fam, int k, int zflag)
+{
+    if (k == 0) {
+        memcpy(out, cur, (size_t)W * H * sizeof(uint16_t));
+        return;
+    }
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            int r = lfmo_residual(cur, prev, W, H, T, fam, k, zflag, x, y);
+            out[(size_t)y * W + x] = symbolize16((int16_t)r);
+        }
+}
+
+/* Predictor_both semantics on one x*y*z volume: z_flag = video_bit & z
+ * (bitwise, klb_imageIO.cpp:1270), previous frame = raw frame z-1. */
+void lfmo_predict_volume(const uint16_t* vol, uint16_t* out, int W, int H, int Z, int T,
+                         int fam, int k, int video)
+{
+    size_t fs = (size_t)W * H;
+    for (int z = 0; z < Z; ++z) {
+        int zf = (video & z) & 1;
+        lfmo_predict_frame(vol + z * fs, z ? vol + (z - 1) * fs : NULL, out + z * fs, W, H, T, fam, k, zf);
+    }
+}
+
+/* Exact inverse of lfmo_predict_frame.  Returns 0, or -1 when the frame is a
+ * temporal frame of the angle/space families (r = ((I-pred)+P)>>1 drops a bit;
+ * the reference inverses lfm_Predictors_space.cu:1349-2049 /
+ * lfm_Predictors_angle.cu:1416-2587 do not invert it either). */
+int lfmo_unpredict_frame(const uint16_t* sym, const uint16_t* prev_dec, uint16_t* out,
+                         int W, int H, int T, int fam, int k, int zflag)
+{
+    if (k == 0) {
+        memcpy(out, sym, (size_t)W * H * sizeof(uint16_t));
+        return 0;
+    }
+    if (zflag && fam != 0) return -1;
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            nbr_t n = {out, W, T, x, y};
+            int tx = x / T, ty = y / T, u = x % T, v = y % T;
+            int tc = tile_case(tx, ty), uc = pos_case(u, v);
+            int f = family_table(fam)[k - 1][tc][uc];
+            int r = (int)unsymbolize16(sym[(size_t)y * W + x]);
+            int pr = pred_formula(f, &n);
+            int val;
+            if (!zflag) val = r + pr;
+            else {
+                int P = (int)prev_dec[(size_t)y * W + x];
+                val = (f == F_Z) ? r + P : r + ((pr + P) >> 1);
+            }
+            out[(size_t)y * W + x] = (uint16_t)val;
+        }
+    return 0;
+}
+
+int lfmo_unpredict_volume(const uint16_t* sym, uint16_t* out, int W, int H, int Z, int T,
+                          int fam, int k, int video)
+{
+    size_t fs = (size_t)W * H;
+    for (int z = 0; z < Z; ++z) {
+        int zf = (video & z) & 1;
+        int rc = lfmo_unpredict_frame(sym + z * fs, z ? out + (z - 1) * fs : NULL, out + z * fs,
+                                      W, H, T, fam, k, zf);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * 2D entropy of one candidate buffer (klb_imageIO.cpp:2030-2093).
+ * Per chunk of n <= 450000 pixels, S = 2n bytes c[0..S):
+ *   bwt_GPU (lfm_Predictors.cu:2883-2914): pairs (key c[i], val c[i-1]) for
+ *     i < S with c[-1] = 0, plus a sentinel (key 0, val c[S-1]); stable sort by
+ *     key -> L[0..S].
+ *   static_bwt_GPU (:2833-2856): h[(L[j] << 8) | L[j+1]] += 1 for j < S.
+ *   sum_bwt_GPU (:2923-2949): sum over bins b < 65535 (bin 0xFFFF is outside
+ *     the reference's 65535-entry allocation and never summed) with h > 0 of
+ *     -P * logf(P), P = (float)h / (float)S.
+ * The chunk sums are accumulated in float in chunk order.
+ * ------------------------------------------------------------------------- */
+float lfmo_entropy_chunk(const uint8_t* c, uint32_t S, uint32_t* hist /* 65536 scratch */)
+{
+    uint32_t cnt[257];
+    memset(cnt, 0, sizeof(cnt));
+    for (uint32_t i = 0; i < S; ++i) cnt[c[i] + 1]++;
+    cnt[0 + 1]++; /* sentinel has key 0 */
+    for (int k = 0; k < 256; ++k) cnt[k + 1] += cnt[k];
+    uint8_t* L = (uint8_t*)malloc((size_t)S + 1);
+    /* stable counting sort: elements in index order, sentinel last (index S) */
+    for (uint32_t i = 0; i < S; ++i) {
+        uint8_t val = i ? c[i - 1] : 0;
+        L[cnt[c[i]]++] = val;
+    }
+    L[cnt[0]++] = S ? c[S - 1] : 0;
+    memset(hist, 0, 65536 * sizeof(uint32_t));
+    for (uint32_t j = 0; j < S; ++j) hist[((uint32_t)L[j] << 8) | L[j + 1]]++;
+    free(L);
+    float e = 0.0f;
+    const float fs = (float)S;
+    for (uint32_t b = 0; b < 65535; ++b) {
+        if (!hist[b]) continue;
+        float P = (float)hist[b] / fs;
+        e += -1 * P * logf(P);
+    }
+    return e;
+}
+
+float lfmo_entropy2d(const uint16_t* cand, uint64_t npix)
+{
+    const uint64_t block = 450000;
+    uint32_t* hist = (uint32_t*)malloc(65536 * sizeof(uint32_t));
+    float acc = 0.0f;
+    for (uint64_t z = 0; z < npix; z += block) {
+        uint64_t n = npix - z < block ? npix - z : block;
+        acc += lfmo_entropy_chunk((const uint8_t*)(cand + z), (uint32_t)(n * 2), hist);
+    }
+    free(hist);
+    return acc;
+}
+
+/* Candidate entropies and the reference's selection rule
+ * (klb_imageIO.cpp:2197-2225, :2300-2305): candidate 0 = raw frame with its
+ * entropy scaled by 0.96 (:2087-2090); candidate k = symbolized residual of
+ * predictor k on the spatial path (z = 0); std::map<float,int> keeps the LAST
+ * index inserted for equal keys, so exact ties go to the highest k. */
+int lfmo_select(const uint16_t* frame, int W, int H, int T, int fam, float ent[8])
+{
+    size_t np = (size_t)W * H;
+    uint16_t* buf = (uint16_t*)malloc(np * sizeof(uint16_t));
+    int best = 0;
+    for (int k = 0; k < 8; ++k) {
+        lfmo_predict_frame(frame, NULL, buf, W, H, T, fam, k, 0);
+        float e = lfmo_entropy2d(buf, np);
+        ent[k] = (k == 0) ? (float)((double)e * 0.96) : e; /* float * double literal */
+    }
+    free(buf);
+    for (int k = 1; k < 8; ++k)
+        if (ent[k] <= ent[best]) best = k;
+    return best;
+}

@@ -1,0 +1,197 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and
+the committed golden fixtures.  Bit-exact for symbols, headers and .lfm bytes;
+entropies within 1e-5 relative (float summation order is unpinned in the
+reference: thrust::reduce)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+FAMS = ["tiles", "angle", "space"]
+
+
+def dev16(torch, a):
+    t = torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda()
+    return t
+
+
+def host16(t):
+    return t.cpu().numpy().view(np.uint16)
+
+
+def run_predict(lfmlib, torch, frames, T, fam, k, video, z0=0, prev=None):
+    Z, H, W = frames.shape
+    d_in = dev16(torch, frames)
+    d_out = torch.empty_like(d_in)
+    d_prev = dev16(torch, prev) if prev is not None else None
+    lfmlib.predict_device(d_in, d_out, W, H, Z, T, fam, k, video, z0, d_prev)
+    torch.cuda.synchronize()
+    return host16(d_out)
+
+
+def test_golden_predictor_vectors(lfmlib, gpu):
+    torch = gpu
+    g = np.load(os.path.join(GOLDEN, "predictor_vectors.npz"))
+    n = 0
+    for key in g.files:
+        if not key.startswith("in_"):
+            continue
+        tag = key[3:]
+        T = int(tag.split("_T")[1])
+        fr = g[key]
+        for fam in FAMS:
+            for k in range(1, 8):
+                sp = run_predict(lfmlib, torch, fr[1:2], T, fam, k, 0)[0]
+                assert np.array_equal(sp, g["%s_%s_k%d_z0" % (tag, fam, k)]), (tag, fam, k, "spatial")
+                # temporal: frame index 1 of a video stack -> z_flag = 1, prev = frame 0
+                tp = run_predict(lfmlib, torch, fr, T, fam, k, 1)[1]
+                assert np.array_equal(tp, g["%s_%s_k%d_z1" % (tag, fam, k)]), (tag, fam, k, "temporal")
+                n += 2
+    assert n > 500
+
+
+@pytest.mark.parametrize("W,H,T", [(512, 256, 13), (2048, 160, 15), (1032, 200, 15), (520, 300, 31), (64, 64, 2),
+                                   (1024, 96, 1), (776, 130, 11)])
+def test_fast_kernel_vs_oracle(lfmlib, oracle, gpu, W, H, T):
+    """Shapes that take the LDS-ring kernel (W % 8 == 0, T <= 31): several
+    strips, partial last strip, several row segments, video stacks."""
+    torch = gpu
+    stack = oracle.synthetic_lf(W, H, Z=4, T=T, seed=W * 7 + H)[0, 0]
+    rng = np.random.default_rng(W + H)
+    stack[2] = rng.integers(0, 65536, size=(H, W), dtype=np.uint16)  # full range exercises the int16 wrap
+    for fam in FAMS:
+        for k in range(1, 8):
+            got = run_predict(lfmlib, torch, stack, T, fam, k, 1)
+            exp = oracle.predict_volume(stack, T, fam, k, 1)
+            assert np.array_equal(got, exp), (fam, k)
+
+
+def test_predict_z0_offset_and_prev(lfmlib, oracle, gpu):
+    """A z-slab starting at an odd z of a video stack takes its previous raw
+    frame from d_prev (multi-GPU slabs use this)."""
+    torch = gpu
+    stack = oracle.synthetic_lf(512, 64, Z=6, T=15)[0, 0]
+    full = oracle.predict_volume(stack, 15, "tiles", 4, 1)
+    got = run_predict(lfmlib, torch, stack[3:], 15, "tiles", 4, 1, z0=3, prev=stack[2:3])
+    assert np.array_equal(got, full[3:])
+
+
+def test_predictor0_is_copy(lfmlib, oracle, gpu):
+    torch = gpu
+    stack = oracle.synthetic_lf(96, 40, Z=2, T=13)[0, 0]
+    assert np.array_equal(run_predict(lfmlib, torch, stack, 13, "tiles", 0, 1), stack)
+
+
+def test_entropy_and_selection_vs_golden(lfmlib, oracle, gpu):
+    torch = gpu
+    rows = json.load(open(os.path.join(GOLDEN, "entropy_vectors.json")))
+    for r in rows:
+        if r["kind"] == "zeros":
+            fr = np.zeros((r["H"], r["W"]), np.uint16)
+        elif r["kind"] == "lf":
+            fr = oracle.synthetic_lf(r["W"], r["H"], Z=2, T=r["T"], seed=r["seed"])[0, 0, 1]
+        else:
+            fr = np.random.default_rng(r["seed"]).integers(0, 65536, size=(2, r["H"], r["W"]), dtype=np.uint16)[1]
+        k, ent = lfmlib.select_device(dev16(torch, fr), r["W"], r["H"], r["T"], r["family"])
+        np.testing.assert_allclose(ent, r["entropy"], rtol=1e-5, atol=1e-6)
+        srt = sorted(r["entropy"])
+        if r["kind"] == "zeros" or srt[1] - srt[0] > 1e-4 * abs(srt[0]):
+            assert k == r["chosen"], r
+
+
+def test_entropy_single_candidate(lfmlib, oracle, gpu):
+    torch = gpu
+    rng = np.random.default_rng(11)
+    for n in (1, 7, 449999, 450000, 450001, 1000003):
+        cand = rng.integers(0, 300, size=n, dtype=np.uint16)
+        e = lfmlib.entropy_device(dev16(torch, cand))
+        assert abs(e - oracle.entropy2d(cand)) <= 1e-5 * max(1.0, abs(e)), n
+
+
+def _manifest():
+    return {e["name"]: e for e in json.load(open(os.path.join(GOLDEN, "lfm_manifest.json")))}
+
+
+def _gen(oracle, e):
+    img_tif = np.load(os.path.join(GOLDEN, "img_tif.npz"))["img"]
+    if e["generator"].startswith("img_tif"):
+        return np.asarray(eval(e["generator"], {"img_tif": img_tif})).reshape(e["shape_tczyx"])
+    return eval("O." + e["generator"], {"O": oracle})
+
+
+@pytest.mark.parametrize("name", ["cfg2_512x512_space_auto", "cfg3s_512x512x8_angle_auto",
+                                  "cfg4s_256x256x16_tiles_auto", "cfg5s_128x128x8x1x3_video_auto",
+                                  "imgtif_page12_auto", "imgtif_stack_auto_video", "matlab_test_m"])
+def test_lfm_bytes_match_oracle_manifest(lfmlib, oracle, gpu, tmp_path, name):
+    """Whole encode (GPU selection + predictor + host bzip2) gives the oracle's
+    .lfm bytes (SHA-256 committed in tests/golden/lfm_manifest.json)."""
+    e = _manifest()[name]
+    img = _gen(oracle, e)
+    lfmlib.set_family(e["family"])
+    try:
+        p = tmp_path / "o.lfm"
+        lfmlib.write_lfm(p, img, predictor_request=e["header_version"] & 0x7F, nnum=e["nnum"],
+                         video=e["header_version"] >> 7, block_size=e["block_size"])
+        b = p.read_bytes()
+        assert b[0] == e["final_header_version"]
+        assert hashlib.sha256(b).hexdigest() == e["sha256"], name
+        # device-resident input through the encoder API gives the same bytes
+        enc = lfmlib.Encoder()
+        t = gpu.from_numpy(np.ascontiguousarray(img).view(np.int16)).cuda()
+        b2, st = enc.encode(t, header_version=e["header_version"], nnum=e["nnum"], block_size=e["block_size"])
+        assert b2 == b and st["chosen"] == (e["final_header_version"] & 0x7F)
+        enc.close()
+        if e["family"] == "tiles" or not (e["header_version"] >> 7):
+            back, _, _ = lfmlib.read_lfm(p)
+            assert np.array_equal(back.reshape(img.shape), img)
+    finally:
+        lfmlib.set_family("tiles")
+
+
+@pytest.mark.parametrize("fam", FAMS)
+def test_forced_predictors_small_files(lfmlib, oracle, gpu, tmp_path, fam):
+    man = _manifest()
+    small = oracle.synthetic_lf(70, 45, Z=3, T=13, seed=0x4C464D06)
+    lfmlib.set_family(fam)
+    try:
+        for k in range(8):
+            e = man["small_%s_req%d" % (fam, 8 + k)]
+            p = tmp_path / ("k%d.lfm" % k)
+            lfmlib.write_lfm(p, small, predictor_request=8 + k, nnum=13, block_size=e["block_size"])
+            assert p.read_bytes() == open(os.path.join(GOLDEN, e["file"]), "rb").read(), (fam, k)
+    finally:
+        lfmlib.set_family("tiles")
+
+
+def test_config3_full_size_properties(lfmlib, oracle, gpu):
+    """Config 3 at full size (2048 x 2048 x 64, Nnum 15, angle, auto on frame 0):
+    the GPU symbols decode back to the input (angle spatial is lossless), and
+    sampled frames equal the oracle bit for bit."""
+    torch = gpu
+    X, Y, Z, T = 2048, 2048, 64, 15
+    d_img = torch.empty((Z, Y, X), dtype=torch.int16, device="cuda")
+    lfmlib.synth_device(d_img, X, Y, Z, T, seed=0x4C464D03)
+    k, ent = lfmlib.select_device(d_img[0], X, Y, T, "angle")
+    f0 = host16(d_img[0])
+    ko, ento = oracle.select(f0, T, "angle")
+    np.testing.assert_allclose(ent, ento, rtol=1e-5)
+    assert k == ko
+    d_sym = torch.empty_like(d_img)
+    lfmlib.predict_device(d_img, d_sym, X, Y, Z, T, "angle", k, 0)
+    torch.cuda.synchronize()
+    for z in (0, 31, 63):
+        assert np.array_equal(host16(d_sym[z]), oracle.predict_frame(host16(d_img[z]), None, T, "angle", k, 0)), z
+
+
+def test_synth_generator_matches_numpy(lfmlib, oracle, gpu):
+    torch = gpu
+    for (X, Y, Z, T) in ((256, 64, 3, 15), (101, 33, 2, 13)):
+        d = torch.empty((Z, Y, X), dtype=torch.int16, device="cuda")
+        lfmlib.synth_device(d, X, Y, Z, T, seed=0x4C464D03)
+        torch.cuda.synchronize()
+        assert np.array_equal(host16(d), oracle.synthetic_lf(X, Y, Z=Z, T=T, seed=0x4C464D03)[0, 0])

@@ -1,0 +1,182 @@
+"""CPU-only tests of liblfm.so: it loads, exports every declared symbol, and
+its host paths (container, block scheduler, bzip2/zlib, decoder) match the oracle."""
+import hashlib
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO
+
+INCLUDE = os.path.join(REPO, "include", "lfm")
+
+
+def declared_c_functions():
+    names = set()
+    for h in ("klb_Cwrapper.h", "lfm_api.h", "lfm_hip.h"):
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*(?:DECLSPECIFIER|LFM_API)?\s*[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\(", src, re.M):
+            name = m.group(1)
+            if name in ("if", "defined", "__attribute__", "visibility"):
+                continue
+            names.add(name)
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol(lfmlib):
+    L = lfmlib.lib()
+    decl = declared_c_functions()
+    assert "writeKLBstack" in decl and "lfm_hip_predict" in decl and "lfm_encoder_encode" in decl
+    missing = [n for n in decl if not hasattr(L, n)]
+    assert missing == []
+    assert lfmlib.missing_exports() == []
+    assert b"gfx950" in L.lfm_version()
+
+
+def test_cpp_class_symbols_exported(lfmlib):
+    """klb_imageIO / klb_image_header (the MEX link surface) are exported."""
+    import subprocess
+    out = subprocess.run(["nm", "-DC", lfmlib.LIB_PATH], capture_output=True, text=True).stdout
+    for sym in ("klb_imageIO::writeImage(char const*, int)", "klb_imageIO::readImageFull(char*, int)",
+                "klb_image_header::setDefaultBlockSize()", "klb_image_header::writeHeader(_IO_FILE*)",
+                "klb_imageIO::readImage(char*, klb_ROI const*, int)"):
+        assert sym in out, sym
+
+
+def _img_tif():
+    return np.load(os.path.join(GOLDEN, "img_tif.npz"))["img"]
+
+
+def _manifest():
+    return {e["name"]: e for e in json.load(open(os.path.join(GOLDEN, "lfm_manifest.json")))}
+
+
+def test_config1_plumbing_bit_identical(lfmlib, tmp_path):
+    """Config 1: img.tif page 0 (all zeros), request 8 (predictor off), default
+    blocks, BZIP2 on the CPU: identical bytes to the oracle's file."""
+    man = _manifest()
+    img = _img_tif()
+    for name, arr in (("cfg1_imgtif_page0_req8", img[0]), ("cfg1_imgtif_stack_req8", img)):
+        p = tmp_path / (name + ".lfm")
+        lfmlib.write_lfm(p, arr, predictor_request=8, nnum=13)
+        b = p.read_bytes()
+        assert hashlib.sha256(b).hexdigest() == man[name]["sha256"], name
+        back, hv, nn = lfmlib.read_lfm(p)
+        assert np.array_equal(back.reshape(arr.shape), arr) and hv == 0 and nn == 13
+
+
+def test_writeKLBstack_defaults_and_readKLB(lfmlib, tmp_path, oracle):
+    """writeKLBstack on 8-bit data: no predictor stage (16-bit only), default blocks."""
+    rng = np.random.default_rng(1)
+    arr = rng.integers(0, 8, size=(3, 50, 70), dtype=np.uint8)
+    p = tmp_path / "u8.klb"
+    lfmlib.write_klb(p, arr, metadata="hello")
+    h = lfmlib.read_header(p)
+    assert h["xyzct"] == [70, 50, 3, 1, 1] and h["data_type"] == 0 and h["block_size"] == [70, 50, 3, 1, 1]
+    assert h["metadata"].startswith(b"hello\0")
+    assert p.read_bytes() == oracle.encode(arr, header_version=0, data_type=0, metadata=b"hello")
+    back, hv, _ = lfmlib.read_lfm(p)
+    assert np.array_equal(back.reshape(arr.shape), arr)
+
+
+@pytest.mark.parametrize("dtype,dt", [(np.float32, 8), (np.int32, 6), (np.uint64, 3)])
+def test_wide_types_roundtrip(lfmlib, tmp_path, oracle, dtype, dt):
+    rng = np.random.default_rng(2)
+    arr = (rng.random((2, 3, 4, 33, 47)) * 100).astype(dtype)
+    p = tmp_path / "w.lfm"
+    lfmlib.write_lfm(p, arr, predictor_request=0, block_size=[16, 16, 3, 2, 1])
+    assert p.read_bytes() == oracle.encode(arr, header_version=0, data_type=dt, block_size=[16, 16, 3, 2, 1])
+    back, _, _ = lfmlib.read_lfm(p)
+    assert np.array_equal(back.reshape(arr.shape), arr)
+
+
+def test_ragged_blocks_5d_raw(lfmlib, tmp_path, oracle):
+    """5-D image, border blocks on every axis, request 8: bytes match the oracle."""
+    img = oracle.synthetic_lf(37, 29, Z=5, C=2, Tn=3, T=7)
+    p = tmp_path / "r.lfm"
+    lfmlib.write_lfm(p, img, predictor_request=8, nnum=7, block_size=[16, 8, 2, 1, 2])
+    assert p.read_bytes() == oracle.encode(img, header_version=8, nnum=7, block_size=[16, 8, 2, 1, 2])
+    back, _, _ = lfmlib.read_lfm(p)
+    assert np.array_equal(back, img)
+
+
+def test_compression_none_and_zlib(lfmlib, tmp_path, oracle):
+    img = oracle.synthetic_lf(40, 30, Z=2, T=13)
+    for ct in (0, 2):
+        p = tmp_path / ("c%d.lfm" % ct)
+        lfmlib.write_lfm(p, img, predictor_request=8, compression=ct)
+        if ct == 0:
+            assert p.read_bytes() == oracle.encode(img, header_version=8, compression=0)
+        back, _, _ = lfmlib.read_lfm(p)
+        assert np.array_equal(back, img)
+
+
+def test_decode_committed_predictor_files(lfmlib):
+    """The product decoder inverts the committed oracle .lfm files (all
+    families, all forced predictors) back to their generator input."""
+    import lfm_oracle as O
+    man = _manifest()
+    small = O.synthetic_lf(70, 45, Z=3, T=13, seed=0x4C464D06)
+    for fam in ("tiles", "angle", "space"):
+        lfmlib.set_family(fam)
+        try:
+            for k in range(8):
+                e = man["small_%s_req%d" % (fam, 8 + k)]
+                b = open(os.path.join(GOLDEN, e["file"]), "rb").read()
+                out = lfmlib.decode(b)
+                assert np.array_equal(out, small), (fam, k)
+        finally:
+            lfmlib.set_family("tiles")
+
+
+def test_decode_video_tiles_file(lfmlib):
+    man = _manifest()
+    b = open(os.path.join(GOLDEN, man["imgtif_stack_auto_video"]["file"]), "rb").read()
+    out = lfmlib.decode(b)
+    assert np.array_equal(out.reshape(_img_tif().shape), _img_tif())
+
+
+def test_roi_read(lfmlib, tmp_path):
+    import ctypes
+    man = _manifest()
+    p = os.path.join(GOLDEN, man["imgtif_stack_auto_video"]["file"])
+    img = _img_tif()
+    lb, ub = [10, 20, 3, 0, 0], [60, 100, 9, 0, 0]
+    out = np.empty((7, 81, 51), np.uint16)
+    rc = lfmlib.lib().readKLBroiInPlace(os.fsencode(p), out.ctypes.data, (ctypes.c_uint32 * 5)(*lb),
+                                         (ctypes.c_uint32 * 5)(*ub), 2)
+    assert rc == 0
+    assert np.array_equal(out, img[3:10, 20:101, 10:61])
+
+
+def test_invalid_predictor_request_rejected(lfmlib, tmp_path):
+    img = np.zeros((1, 16, 16), np.uint16)
+    with pytest.raises(lfmlib.LfmError, match="code 6"):
+        lfmlib.write_lfm(tmp_path / "bad.lfm", img, predictor_request=16)
+
+
+def test_gpu_required_for_predictor_stage(lfmlib, tmp_path):
+    if lfmlib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    img = np.ones((1, 16, 16), np.uint16)
+    with pytest.raises(lfmlib.LfmError, match="code 7"):
+        lfmlib.write_lfm(tmp_path / "x.lfm", img, predictor_request=0)
+    with pytest.raises(lfmlib.LfmError, match="code 7"):
+        lfmlib.write_lfm(tmp_path / "y.lfm", img, predictor_request=9)
+
+
+def test_unopenable_output(lfmlib):
+    with pytest.raises(lfmlib.LfmError, match="code 5"):
+        lfmlib.write_lfm("/nonexistent_dir/x.lfm", np.zeros((4, 4), np.uint16), predictor_request=8)
+
+
+def test_family_switch(lfmlib):
+    assert lfmlib.get_family() == 0
+    lfmlib.set_family("space")
+    assert lfmlib.get_family() == 2
+    lfmlib.set_family("tiles")
+    with pytest.raises(lfmlib.LfmError):
+        lfmlib.set_family(5)

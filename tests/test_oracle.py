@@ -1,0 +1,200 @@
+"""CPU tests of the oracle (test infrastructure) and of its pins to the reference."""
+import hashlib
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REFERENCE, REPO
+
+KAT = os.path.join(GOLDEN, "bzip2_kat")
+
+
+@pytest.mark.parametrize("i,level", [(1, 1), (2, 2), (3, 3)])
+def test_bzip2_known_answers(oracle, i, level):
+    """bzip2-1.0.6 Makefile:56-69 KATs: the oracle's bzip2 and python's bz2
+    (system libbz2, the library liblfm links) both reproduce sample*.bz2."""
+    src = open(os.path.join(KAT, "sample%d.ref" % i), "rb").read()
+    exp = open(os.path.join(KAT, "sample%d.bz2" % i), "rb").read()
+    assert oracle.bzip2().compress(src, level) == exp
+    assert oracle._PyBz2().compress(src, level) == exp
+    assert oracle.bzip2().decompress(exp, len(src)) == src
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REFERENCE, "src")), reason="reference tree absent")
+def test_audit_tables_against_reference_text(oracle):
+    import audit_tables
+    n, bad = audit_tables.audit(REFERENCE)
+    assert n == 672
+    assert bad == []
+
+
+def test_audit_kernel_tables_match_oracle_tables(oracle):
+    """The product's own case tables (lfm_cases.h) equal the oracle's."""
+    import re
+    src = open(os.path.join(REPO, "lightfieldmicroscopy_pc-bzip2_amd", "csrc", "lfm_cases.h")).read()
+    lib = oracle.lib()
+    for fam, name in enumerate(["kTiles", "kAngle", "kSpace"]):
+        body = src[src.index("constexpr uint8_t %s" % name):]
+        body = body[:body.index("};")]
+        ids = re.findall(r"F_[A-Z0-9_]+", body)
+        enum = src[src.index("enum Formula"):src.index("F_COUNT")]
+        order = re.findall(r"F_[A-Z0-9_]+", enum)
+        ocsrc = open(os.path.join(REPO, "oracle", "lfm_oracle.c")).read()
+        oenum = re.findall(r"\b(F_[A-Z0-9_]+)\b", re.sub(r"/\*.*?\*/", "", ocsrc[ocsrc.index("enum {"):ocsrc.index("F_NUM")], flags=re.S))
+        assert order == oenum
+        assert len(ids) == 7 * 16
+        for k in range(7):
+            for tc in range(4):
+                for uc in range(4):
+                    assert order.index(ids[k * 16 + tc * 4 + uc]) == lib.lfmo_case_formula(fam, k + 1, tc, uc)
+
+
+@pytest.mark.parametrize("fam", ["tiles", "angle", "space"])
+def test_oracle_roundtrip(oracle, fam):
+    img = oracle.synthetic_lf(61, 47, Z=4, T=13)[0, 0]
+    for k in range(8):
+        for video in (0, 1):
+            s = oracle.predict_volume(img, 13, fam, k, video)
+            if video and fam != "tiles" and k > 0:
+                with pytest.raises(ValueError):
+                    oracle.unpredict_volume(s, 13, fam, k, video)
+                continue
+            assert np.array_equal(oracle.unpredict_volume(s, 13, fam, k, video), img)
+
+
+def test_oracle_roundtrip_full_range(oracle):
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 65536, size=(3, 40, 52), dtype=np.uint16)
+    for k in range(1, 8):
+        s = oracle.predict_volume(img, 5, "tiles", k, 1)
+        assert np.array_equal(oracle.unpredict_volume(s, 5, "tiles", k, 1), img)
+
+
+def test_symbolize_bijective(oracle):
+    L = oracle.lib()
+    import ctypes
+    L.lfmo_symbolize.restype = ctypes.c_uint16
+    L.lfmo_symbolize.argtypes = [ctypes.c_int16]
+    L.lfmo_unsymbolize.restype = ctypes.c_int16
+    L.lfmo_unsymbolize.argtypes = [ctypes.c_uint16]
+    seen = set()
+    for r in list(range(-32768, -32700)) + list(range(-300, 300)) + list(range(32700, 32768)):
+        s = L.lfmo_symbolize(r)
+        assert L.lfmo_unsymbolize(s) == r
+        seen.add(s)
+    assert L.lfmo_symbolize(-32768) == 65535
+    assert L.lfmo_symbolize(0) == 0 and L.lfmo_symbolize(-1) == 1 and L.lfmo_symbolize(1) == 2
+
+
+def test_golden_predictor_vectors(oracle):
+    g = np.load(os.path.join(GOLDEN, "predictor_vectors.npz"))
+    n = 0
+    for key in g.files:
+        if not key.startswith("in_"):
+            continue
+        tag = key[3:]
+        T = int(tag.split("_T")[1])
+        fr = g[key]
+        for fam in ("tiles", "angle", "space"):
+            for k in range(1, 8):
+                assert np.array_equal(oracle.predict_frame(fr[1], None, T, fam, k, 0), g["%s_%s_k%d_z0" % (tag, fam, k)])
+                assert np.array_equal(oracle.predict_frame(fr[1], fr[0], T, fam, k, 1), g["%s_%s_k%d_z1" % (tag, fam, k)])
+                n += 2
+    assert n > 500
+
+
+def test_golden_entropy_vectors(oracle):
+    rows = json.load(open(os.path.join(GOLDEN, "entropy_vectors.json")))
+    for r in rows[:9]:
+        if r["kind"] == "zeros":
+            fr = np.zeros((r["H"], r["W"]), np.uint16)
+        elif r["kind"] == "lf":
+            fr = oracle.synthetic_lf(r["W"], r["H"], Z=2, T=r["T"], seed=r["seed"])[0, 0, 1]
+        else:
+            fr = np.random.default_rng(r["seed"]).integers(0, 65536, size=(2, r["H"], r["W"]), dtype=np.uint16)[1]
+        k, ent = oracle.select(fr, r["T"], r["family"])
+        assert k == r["chosen"]
+        np.testing.assert_allclose(ent, r["entropy"], rtol=1e-6)
+
+
+def test_selection_tie_rule_all_zero(oracle):
+    """An all-zero frame gives 8 exactly-equal entropies (0); std::map keeps
+    the last index inserted -> predictor 7 (klb_imageIO.cpp:2300-2305)."""
+    k, ent = oracle.select(np.zeros((30, 30), np.uint16), 13, "tiles")
+    assert k == 7 and np.all(ent == 0)
+
+
+def test_entropy_matches_direct_definition(oracle):
+    """The stable-sort + bigram restatement equals the pair-list definition."""
+    rng = np.random.default_rng(3)
+    cand = rng.integers(0, 40, size=777, dtype=np.uint16)
+    c = cand.view(np.uint8)
+    S = c.size
+    keys = list(c) + [0]
+    vals = [0] + list(c[:-1]) + [c[-1]]
+    order = sorted(range(S + 1), key=lambda i: (keys[i], i))
+    L = [vals[i] for i in order]
+    h = {}
+    for j in range(S):
+        b = (int(L[j]) << 8) | int(L[j + 1])
+        h[b] = h.get(b, 0) + 1
+    e = np.float32(0)
+    for b in sorted(h):
+        if b == 0xFFFF:
+            continue
+        P = np.float32(h[b]) / np.float32(S)
+        e += np.float32(-1) * P * np.log(P, dtype=np.float32)
+    assert abs(oracle.entropy2d(cand) - float(e)) < 1e-5
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REPO, "oracle", "_ref", "libklbheader_ref.so")),
+                    reason="reference header library not built")
+def test_header_bytes_match_reference_class(oracle):
+    """oracle.header_bytes == the reference's klb_image_header::writeHeader(FILE*)."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "libklbheader_ref.so"))
+    xyzct = [101, 151, 29, 1, 1]
+    bs = [96, 96, 8, 1, 1]
+    nb = int(np.prod(oracle.num_blocks_per_dim(xyzct, bs)))
+    offs = np.arange(1, nb + 1, dtype=np.uint64) * 1000
+    md = b"test".ljust(256, b"\0")
+    out = ctypes.create_string_buffer(4096)
+    n = L.ref_header_bytes((ctypes.c_uint32 * 5)(*xyzct), 1, (ctypes.c_float * 5)(1, 1, 2.5, 1, 1),
+                           (ctypes.c_uint32 * 5)(*bs), 1, md, 0x85, 15,
+                           offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ctypes.c_size_t(nb), out, 4096)
+    assert n == 320 + 8 * nb
+    mine = oracle.header_bytes(0x85, 15, xyzct, [1, 1, 2.5, 1, 1], 1, 1, md, bs, offs)
+    assert out.raw[:n] == mine
+
+
+def test_lfm_manifest_small_files(oracle):
+    """Committed small .lfm fixtures decode to their generator input and re-encode identically."""
+    man = json.load(open(os.path.join(GOLDEN, "lfm_manifest.json")))
+    img_tif = np.load(os.path.join(GOLDEN, "img_tif.npz"))["img"]
+    for e in man:
+        if "file" not in e:
+            continue
+        b = open(os.path.join(GOLDEN, e["file"]), "rb").read()
+        assert hashlib.sha256(b).hexdigest() == e["sha256"]
+        img, h = oracle.decode(b, family=e["family"])
+        gen = e["generator"]
+        if gen.startswith("img_tif"):
+            src = eval(gen, {"img_tif": img_tif})
+        else:
+            src = eval("O." + gen, {"O": oracle})
+        src = np.asarray(src).reshape(img.shape)
+        assert np.array_equal(img, src), e["name"]
+        b2 = oracle.encode(src, header_version=e["header_version"], nnum=e["nnum"], family=e["family"],
+                           block_size=e["block_size"])
+        assert b2 == b, e["name"]
+
+
+def test_header_layout_fields(oracle):
+    b = open(os.path.join(GOLDEN, "lfm_small", "matlab_test_m.lfm"), "rb").read()
+    hv, nnum = struct.unpack_from("<BB", b, 0)
+    assert (hv, nnum) == (7, 13)
+    h = oracle.parse_header(b)
+    assert h["xyzct"] == [101, 151, 1, 1, 1] and h["nb"] == 1 and h["offsets"][-1] == len(b) - 328
