@@ -155,17 +155,21 @@ __host__ __device__ __forceinline__ int eval_formula(G& g)
 template <int FAM, int K, int TC, int UC, bool TEMPORAL, class G>
 __host__ __device__ __forceinline__ int case_residual(G& g, int I, int P)
 {
-    constexpr int F = case_formula(FAM, K, TC, UC);
-    if constexpr (!TEMPORAL) {
-        return I - eval_formula<F>(g);
-    } else if constexpr (F == F_Z) {
-        return I - P;
-    } else if constexpr (FAM == 0) {
-        return I - ((eval_formula<F>(g) + P) >> 1);
-    } else if constexpr (temporal_twice(FAM, K, TC, UC)) {
-        return ((((I - eval_formula<F>(g)) + P) >> 1) + P) >> 1;
+    if constexpr (K < 1) {  // predictor 0 (raw) / diagnostic builds
+        return I;
     } else {
-        return ((I - eval_formula<F>(g)) + P) >> 1;
+        constexpr int F = case_formula(FAM, K, TC, UC);
+        if constexpr (!TEMPORAL) {
+            return I - eval_formula<F>(g);
+        } else if constexpr (F == F_Z) {
+            return I - P;
+        } else if constexpr (FAM == 0) {
+            return I - ((eval_formula<F>(g) + P) >> 1);
+        } else if constexpr (temporal_twice(FAM, K, TC, UC)) {
+            return ((((I - eval_formula<F>(g)) + P) >> 1) + P) >> 1;
+        } else {
+            return ((I - eval_formula<F>(g)) + P) >> 1;
+        }
     }
 }
 

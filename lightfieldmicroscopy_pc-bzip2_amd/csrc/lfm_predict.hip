@@ -22,17 +22,15 @@
 // +2 B read on temporal frames.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "lfm_cases.h"
 #include "lfm_hip.h"
 
 namespace lfm {
 
 constexpr int kStrip = 512;           // pixels per strip (64 lanes x 8)
-constexpr int kHalo = 32;             // left halo pixels (covers x - T - 1 for T <= 31)
-constexpr int kSlot = kHalo + kStrip; // pixels per LDS row slot (1088 bytes)
-constexpr int kWaves = 4;
-constexpr int kThreads = kWaves * 64;
-constexpr int kPrefetch = 2;          // steps of rows kept in flight per wave
+// LDS row slot = left halo + 512 strip pixels; the halo covers x - T - 1:
+// 16 pixels for Nnum <= 15, 32 for Nnum <= 31 (runtime, see launch_k)
 constexpr int kMaxFastT = 31;
 
 struct FrameSet {
@@ -40,6 +38,7 @@ struct FrameSet {
     const uint16_t* prev;  // raw frame preceding in[0] (needed if frame 0 is temporal) or null
     uint16_t* out;         // symbols, same layout
     int W, H, T, nz, z0, video;
+    int halo;  // fast kernel only: left halo pixels of an LDS row slot
 };
 
 __device__ __forceinline__ bool frame_temporal(const FrameSet& p, int fz)
@@ -118,118 +117,310 @@ __global__ __launch_bounds__(256) void predict_generic(FrameSet p)
 }
 
 // -------------------------------------------------------------- fast path --
-struct RingNb {
-    const uint16_t* ring;
-    int s0, s1, sT, sT1;  // LDS offsets (pixels) of rows y, y-1, y-T, y-T-1 at column c
+// Per-lane pointers into the LDS ring for the four rows a pixel can reach
+// (y, y-1, y-T, y-T-1), already offset by the lane's column; pixel group j of
+// a lane is 64*j columns further, so every neighbour read below is a
+// ds_read_u16 with an immediate offset off one of these bases.
+struct RowPtrs {
+    const uint16_t* q0;
+    const uint16_t* q1;
+    const uint16_t* qT;
+    const uint16_t* qT1;
     int T;
+};
+
+template <int J>
+struct PxNb {
+    const RowPtrs& r;
     template <int N>
     __device__ __forceinline__ int at() const
     {
-        if constexpr (N == NB_A) return ring[s0 - 1];
-        if constexpr (N == NB_B) return ring[s1];
-        if constexpr (N == NB_C) return ring[s1 - 1];
-        if constexpr (N == NB_AP) return ring[s0 - T];
-        if constexpr (N == NB_BP) return ring[sT];
-        if constexpr (N == NB_CP) return ring[sT - T];
-        if constexpr (N == NB_AP1) return ring[s0 - T - 1];
-        if constexpr (N == NB_BP1) return ring[sT1];
-        if constexpr (N == NB_ABP) return ring[sT - 1];
-        if constexpr (N == NB_BAP) return ring[s1 - T];
+        constexpr int o = J * 64;
+        if constexpr (N == NB_A) return r.q0[o - 1];
+        if constexpr (N == NB_B) return r.q1[o];
+        if constexpr (N == NB_C) return r.q1[o - 1];
+        if constexpr (N == NB_AP) return r.q0[o - r.T];
+        if constexpr (N == NB_BP) return r.qT[o];
+        if constexpr (N == NB_CP) return r.qT[o - r.T];
+        if constexpr (N == NB_AP1) return r.q0[o - r.T - 1];
+        if constexpr (N == NB_BP1) return r.qT1[o];
+        if constexpr (N == NB_ABP) return r.qT[o - 1];
+        if constexpr (N == NB_BAP) return r.q1[o - r.T];
         return 0;
     }
 };
 
-// residual of one pixel inside a row whose (ty==0, v==0) pair is fixed
-template <int FAM, int K, bool TEMP, bool TY0, bool V0>
-__device__ __forceinline__ int row_residual(RingNb& g, int I, int P, bool u0, bool tx0)
-{
-    constexpr int tcX = TY0 ? TC_X0 : TC_XY;
-    constexpr int tc0 = TY0 ? TC_00 : TC_0Y;
-    constexpr int ucU = V0 ? UC_CORNER : UC_COL;
-    constexpr int ucI = V0 ? UC_ROW : UC_IN;
-    int r_in = case_residual<FAM, K, tcX, ucI, TEMP>(g, I, P);
-    int r_u0 = case_residual<FAM, K, tcX, ucU, TEMP>(g, I, P);
-    int r = u0 ? r_u0 : r_in;
-    if (tx0) {  // only lanes of strip 0 with x < T (wave-divergent but rare)
-        r = u0 ? case_residual<FAM, K, tc0, ucU, TEMP>(g, I, P) : case_residual<FAM, K, tc0, ucI, TEMP>(g, I, P);
+// runtime-case neighbour accessor for the rare rows / columns
+struct PxNbDyn {
+    const RowPtrs& r;
+    int o;
+    template <int N>
+    __device__ __forceinline__ int at() const
+    {
+        if constexpr (N == NB_A) return r.q0[o - 1];
+        if constexpr (N == NB_B) return r.q1[o];
+        if constexpr (N == NB_C) return r.q1[o - 1];
+        if constexpr (N == NB_AP) return r.q0[o - r.T];
+        if constexpr (N == NB_BP) return r.qT[o];
+        if constexpr (N == NB_CP) return r.qT[o - r.T];
+        if constexpr (N == NB_AP1) return r.q0[o - r.T - 1];
+        if constexpr (N == NB_BP1) return r.qT1[o];
+        if constexpr (N == NB_ABP) return r.qT[o - 1];
+        if constexpr (N == NB_BAP) return r.q1[o - r.T];
+        return 0;
     }
-    return r;
-}
+};
 
-template <int FAM, int K, bool TEMP, bool TY0, bool V0>
-__device__ __forceinline__ void compute_row(const FrameSet& p, const uint16_t* ring, int slot_y, int slot_y1,
-                                            int slot_yT, int slot_yT1, int y, int xs, int lane,
-                                            const uint16_t* prevf, uint16_t* outf)
+// Any row, any strip: full per-pixel case logic (rows y < T, the last partial
+// strip).  Correct everywhere, used only where the fast row does not apply.
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ void slow_row(const RowPtrs& r, int y, int xs, int W, int lane, const uint16_t* prow,
+                                         uint16_t* orow)
 {
-#pragma unroll
+    if constexpr (K == 0) return;
+    const int T = r.T;
+    const int ty = y / T, v = y - ty * T;
     for (int j = 0; j < kStrip / 64; ++j) {
         const int c = j * 64 + lane;
         const int x = xs + c;
-        if (x < p.W) {
-            const int cc = kHalo + c;
-            RingNb g{ring, slot_y + cc, slot_y1 + cc, slot_yT + cc, slot_yT1 + cc, p.T};
-            const int I = ring[slot_y + cc];
-            const int P = TEMP ? (int)prevf[(size_t)y * p.W + x] : 0;
-            const bool u0 = (x % p.T) == 0;
-            const bool tx0 = x < p.T;
-            int r = row_residual<FAM, K, TEMP, TY0, V0>(g, I, P, u0, tx0);
-            outf[(size_t)y * p.W + x] = (uint16_t)symbolize16(r);
+        if (x >= W) break;
+        PxNbDyn g{r, j * 64};
+        const int tx = x / T, u = x - tx * T;
+        const int I = r.q0[j * 64];
+        const int P = TEMP ? (int)prow[j * 64] : 0;
+        const int res = residual_any_case<FAM, K, TEMP>(g, tile_case(tx, ty), pos_case(u, v), I, P);
+        orow[j * 64] = (uint16_t)symbolize16(res);
+    }
+}
+
+// Rows y >= T of full strips: tile case is TC_XY except the columns x < T of
+// strip 0 (TC_0Y); the position case is fixed by (u == 0, v == 0).
+template <int FAM, int K, bool TEMP, bool V0, bool FIRST, int J>
+__device__ __forceinline__ void fast_px(const RowPtrs& r, uint32_t u0bits, int lane, const uint16_t* prow,
+                                        uint16_t* orow)
+{
+    constexpr int ucU = V0 ? UC_CORNER : UC_COL;
+    constexpr int ucI = V0 ? UC_ROW : UC_IN;
+    PxNb<J> g{r};
+    const int I = r.q0[J * 64];
+    const int P = TEMP ? (int)prow[J * 64] : 0;
+    if constexpr (K == 0) {  // diagnostic ablation: same loads / LDS / stores, no prediction
+        orow[J * 64] = (uint16_t)(I + P);
+        return;
+    }
+    // both candidates are evaluated and blended with a mask: no divergent branch
+    const int m0 = -(int)((u0bits >> J) & 1u);
+    const int r_u = case_residual<FAM, K, TC_XY, ucU, TEMP>(g, I, P);
+    const int r_i = case_residual<FAM, K, TC_XY, ucI, TEMP>(g, I, P);
+    int res = r_i ^ ((r_u ^ r_i) & m0);
+    if constexpr (FIRST && J == 0) {
+        const int mt = -(int)(lane < r.T);  // x < T: first lens column
+        const int t_u = case_residual<FAM, K, TC_0Y, ucU, TEMP>(g, I, P);
+        const int t_i = case_residual<FAM, K, TC_0Y, ucI, TEMP>(g, I, P);
+        const int rt = t_i ^ ((t_u ^ t_i) & m0);
+        res = res ^ ((rt ^ res) & mt);
+    }
+    orow[J * 64] = (uint16_t)symbolize16(res);
+}
+
+template <int FAM, int K, bool TEMP, bool V0, bool FIRST>
+__device__ __forceinline__ void fast_row(const RowPtrs& r, uint32_t u0bits, int lane, const uint16_t* prow,
+                                         uint16_t* orow)
+{
+    fast_px<FAM, K, TEMP, V0, FIRST, 0>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 1>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 2>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 3>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 4>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 5>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 6>(r, u0bits, lane, prow, orow);
+    fast_px<FAM, K, TEMP, V0, FIRST, 7>(r, u0bits, lane, prow, orow);
+}
+
+// sy = slot of row y in the ring (y mod R), v = y mod T, both tracked
+// incrementally by the caller (no integer division per row).  prow: P-ring
+// slot of row y (temporal frames).
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ void compute_row(const FrameSet& p, const uint16_t* ring, int R, int y, int sy, int v,
+                                            int xs, int lane, bool full, uint32_t u0bits, const uint16_t* prow,
+                                            uint16_t* outf)
+{
+    const int T = p.T;
+    auto wrap = [&](int s) { return s < 0 ? s + R : s; };
+    const int slot = p.halo + kStrip;
+    const uint16_t* r0 = ring + sy * slot;
+    const uint16_t* r1 = ring + wrap(sy - 1) * slot;
+    const uint16_t* rT = ring + wrap(sy - T) * slot;
+    const uint16_t* rT1 = ring + wrap(sy - T - 1) * slot;
+    uint16_t* orow0 = outf + (size_t)y * p.W + xs;
+    if (!full || y < T) {
+        const int h = p.halo + lane;
+        const RowPtrs r{r0 + h, r1 + h, rT + h, rT1 + h, T};
+        slow_row<FAM, K, TEMP>(r, y, xs, p.W, lane, TEMP ? prow + lane : nullptr, orow0 + lane);
+        return;
+    }
+    const bool first = xs == 0;
+    const int h = p.halo + lane;
+    const RowPtrs r{r0 + h, r1 + h, rT + h, rT1 + h, T};
+    const uint16_t* pr = TEMP ? prow + lane : nullptr;
+    if (v == 0) {
+        if (first) fast_row<FAM, K, TEMP, true, true>(r, u0bits, lane, pr, orow0 + lane);
+        else fast_row<FAM, K, TEMP, true, false>(r, u0bits, lane, pr, orow0 + lane);
+    } else {
+        if (first) fast_row<FAM, K, TEMP, false, true>(r, u0bits, lane, pr, orow0 + lane);
+        else fast_row<FAM, K, TEMP, false, false>(r, u0bits, lane, pr, orow0 + lane);
+    }
+}
+
+// LDS-DMA (global_load_lds_dwordx4: 16 B per lane into LDS at M0 + 16*lane),
+// issued from inline asm so the compiler's waitcnt pass does not treat every
+// later ds_read of the computing waves as a reader of an in-flight DMA (it
+// would insert vmcnt(0) there, i.e. wait for the wave's own stores).  The
+// loader wave counts its DMAs itself (wait_vmcnt below).
+__device__ __forceinline__ void glds16(const void* g, const void* lds)
+{
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(g)
+                 : "memory", "m0");
+}
+
+// Loader wave: one LDS-DMA (global_load_lds_dwordx4, 16 B per lane, 1 KiB per
+// instruction) for the 512 strip pixels of a row and one for its 32-pixel left
+// halo (lanes 0-3).  Addresses are clamped to valid pixels so the count of
+// instructions per row never changes (the vmcnt waits below are counted).
+__device__ __forceinline__ void dma_row(uint16_t* ring, int slot_idx, const uint16_t* f, int W, int halo,
+                                        int src_row, int xs, int lane)
+{
+    uint16_t* slot = ring + slot_idx * (halo + kStrip);
+    const uint16_t* srow = f + (size_t)src_row * W;
+    const int x = min(xs + lane * 8, W - 8);
+    glds16(srow + x, slot + halo);
+    if (lane < halo / 8) {
+        const int hx = xs > 0 ? xs - halo + lane * 8 : lane * 8;
+        glds16(srow + hx, slot);
+    }
+}
+
+__device__ __forceinline__ void dma_prev_row(uint16_t* pring, int pslot_idx, const uint16_t* pf, int W, int src_row,
+                                             int xs, int lane)
+{
+    uint16_t* slot = pring + pslot_idx * kStrip;
+    const int x = min(xs + lane * 8, W - 8);
+    glds16(pf + (size_t)src_row * W + x, slot);
+}
+
+// rows ys+4s .. ys+4s+3; slot0 / pslot0 = ring slots of row ys+4s
+template <int NCW, bool TEMP>
+__device__ __forceinline__ void dma_step(uint16_t* ring, int R, int slot0, uint16_t* pring, int RP, int pslot0,
+                                         const uint16_t* f, const uint16_t* pf, int W, int halo, int ys, int ye, int s,
+                                         int xs, int lane)
+{
+#pragma unroll
+    for (int i = 0; i < NCW; ++i) {
+        const int row = ys + s * NCW + i;
+        const int src = min(row, ye - 1);
+        int si = slot0 + i;
+        si = si >= R ? si - R : si;
+        dma_row(ring, si, f, W, halo, src, xs, lane);
+        if constexpr (TEMP) {
+            int pi = pslot0 + i;
+            pi = pi >= RP ? pi - RP : pi;
+            dma_prev_row(pring, pi, pf, W, src, xs, lane);
         }
     }
 }
 
-template <int FAM, int K, bool TEMP>
-__device__ __forceinline__ void compute_row_dispatch(const FrameSet& p, const uint16_t* ring, int R, int y, int xs,
-                                                     int lane, const uint16_t* prevf, uint16_t* outf)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
 {
+    static_assert(N >= 0 && N < 64, "vmcnt field is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One work item (frame, row segment, strip) of the workgroup: waves 0-3
+// compute rows ys+4s+wave, wave 4 streams rows PD steps ahead into the ring.
+template <int FAM, int K, int NCW, int RPW, int PD, bool TEMP>
+__device__ __forceinline__ void ring_item(const FrameSet& p, uint16_t* ring, int R, uint16_t* pring, int RP,
+                                          const uint16_t* f, const uint16_t* pf, uint16_t* outf, int xs, int ys,
+                                          int ye, int wave, int lane)
+{
+    constexpr int RS = NCW * RPW;  // rows per step; compute wave w owns rows w, w+NCW, ... of the step
+    constexpr int kLoadsPerStep = RS * (TEMP ? 3 : 2);
+    const bool loader = wave == NCW;
+    const int nsteps = (ye - ys + RS - 1) / RS;
+    const bool full = xs + kStrip <= p.W;
     const int T = p.T;
-    auto slot = [&](int yy) { int s = yy % R; return (s < 0 ? s + R : s) * kSlot; };
-    const int s0 = slot(y), s1 = slot(y - 1), sT = slot(y - T), sT1 = slot(y - T - 1);
-    const bool ty0 = y < T;
-    const bool v0 = (y % T) == 0;
-    if (ty0) {
-        if (v0) compute_row<FAM, K, TEMP, true, true>(p, ring, s0, s1, sT, sT1, y, xs, lane, prevf, outf);
-        else compute_row<FAM, K, TEMP, true, false>(p, ring, s0, s1, sT, sT1, y, xs, lane, prevf, outf);
+    auto adv = [](int v, int d, int m) { v += d; while (v >= m) v -= m; return v; };
+    uint32_t u0bits = 0;  // bit j: column xs + 64j + lane starts a lens (u == 0)
+    // compute waves: row y = ys + wave + 4s, its ring slot, its P slot, y mod T
+    int y = ys + wave, sy = 0, py = 0, vy = 0;
+    // loader: ring / P slots of the first row of step s + PD
+    int lslot = 0, lpslot = 0;
+    if (!loader) {
+#pragma unroll
+        for (int j = 0; j < kStrip / 64; ++j) u0bits |= (uint32_t)(((xs + j * 64 + lane) % T) == 0) << j;
+        sy = y % R;
+        py = TEMP ? y % RP : 0;
+        vy = y % T;
     } else {
-        if (v0) compute_row<FAM, K, TEMP, false, true>(p, ring, s0, s1, sT, sT1, y, xs, lane, prevf, outf);
-        else compute_row<FAM, K, TEMP, false, false>(p, ring, s0, s1, sT, sT1, y, xs, lane, prevf, outf);
+        const int r0 = max(0, ys - T - 1);
+        int ps = r0 % R;
+        for (int row = r0; row < ys; ++row) {
+            dma_row(ring, ps, f, p.W, p.halo, row, xs, lane);
+            ps = ps + 1 == R ? 0 : ps + 1;
+        }
+        int slot0 = ys % R, pslot0 = TEMP ? ys % RP : 0;
+        for (int s = 0; s < PD && s < nsteps; ++s) {
+            dma_step<RS, TEMP>(ring, R, slot0, pring, RP, pslot0, f, pf, p.W, p.halo, ys, ye, s, xs, lane);
+            slot0 = adv(slot0, RS, R);
+            if (TEMP) pslot0 = adv(pslot0, RS, RP);
+        }
+        lslot = slot0;
+        lpslot = pslot0;
     }
+    for (int s = 0; s < nsteps; ++s) {
+        if (loader) {
+            if (s + PD < nsteps) wait_vmcnt<kLoadsPerStep * (PD - 1)>();
+            else wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (loader) {
+            if (s + PD < nsteps) {
+                dma_step<RS, TEMP>(ring, R, lslot, pring, RP, lpslot, f, pf, p.W, p.halo, ys, ye, s + PD, xs, lane);
+                lslot = adv(lslot, RS, R);
+                if (TEMP) lpslot = adv(lpslot, RS, RP);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                if (y < ye) {
+                    const uint16_t* prow = TEMP ? pring + py * kStrip : nullptr;
+                    compute_row<FAM, K, TEMP>(p, ring, R, y, sy, vy, xs, lane, full, u0bits, prow, outf);
+                }
+                y += NCW;
+                sy = adv(sy, NCW, R);
+                if (TEMP) py = adv(py, NCW, RP);
+                vy = adv(vy, NCW, T);
+            }
+        }
+    }
+    // every wave is done reading the ring before the next item's loads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 }
 
-struct RowChunk {
-    uint4 main;
-    uint4 halo;
-};
-
-__device__ __forceinline__ RowChunk load_row(const uint16_t* f, int W, int y, int xs, int lane)
+template <int FAM, int K, int NCW, int RPW, int PD>
+__global__ __launch_bounds__(NCW * 64 + 64) void predict_ring(FrameSet p, int rows_per_seg, int nseg, int nstrip,
+                                                              int R, int RP)
 {
-    RowChunk rc;
-    rc.main = make_uint4(0, 0, 0, 0);
-    rc.halo = make_uint4(0, 0, 0, 0);
-    const uint16_t* row = f + (size_t)y * W;
-    const int x = xs + lane * 8;
-    if (x < W) rc.main = *reinterpret_cast<const uint4*>(row + x);
-    if (lane < kHalo / 8 && xs > 0) rc.halo = *reinterpret_cast<const uint4*>(row + xs - kHalo + lane * 8);
-    return rc;
-}
-
-__device__ __forceinline__ void store_row_lds(uint16_t* ring, int R, int y, int lane, const RowChunk& rc)
-{
-    uint16_t* s = ring + (y % R) * kSlot;
-    *reinterpret_cast<uint4*>(s + kHalo + lane * 8) = rc.main;
-    if (lane < kHalo / 8) *reinterpret_cast<uint4*>(s + lane * 8) = rc.halo;
-}
-
-template <int FAM, int K>
-__global__ __launch_bounds__(kThreads) void predict_fast(FrameSet p, int rows_per_seg, int nseg, int nstrip)
-{
-    extern __shared__ __attribute__((aligned(16))) uint16_t ring[];
-    const int R = p.T + 9;  // rows y-T-1 .. y+3 live during a step, plus the 4 being written
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    uint16_t* ring = lds;
+    uint16_t* pring = lds + R * (p.halo + kStrip);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const size_t fs = (size_t)p.W * p.H;
     const int items = p.nz * nseg * nstrip;
-
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
         const int strip = item % nstrip;
         const int seg = (item / nstrip) % nseg;
@@ -239,39 +430,10 @@ __global__ __launch_bounds__(kThreads) void predict_fast(FrameSet p, int rows_pe
         const int ye = min(ys + rows_per_seg, p.H);
         const uint16_t* f = p.in + (size_t)fz * fs;
         uint16_t* outf = p.out + (size_t)fz * fs;
-        const bool temporal = frame_temporal(p, fz);
-        const uint16_t* prevf = temporal ? frame_prev(p, fz) : nullptr;
-
-        __syncthreads();  // previous item's readers are done with the ring
-        // prime rows ys-T-1 .. ys-1
-        for (int y = max(0, ys - p.T - 1) + wave; y < ys; y += kWaves) {
-            RowChunk rc = load_row(f, p.W, y, xs, lane);
-            store_row_lds(ring, R, y, lane, rc);
-        }
-        RowChunk pf[kPrefetch];
-#pragma unroll
-        for (int d = 0; d < kPrefetch; ++d) {
-            const int y = ys + d * kWaves + wave;
-            if (y < ye) pf[d] = load_row(f, p.W, y, xs, lane);
-        }
-        const int nsteps = (ye - ys + kWaves - 1) / kWaves;
-        for (int s0 = 0; s0 < nsteps; s0 += kPrefetch) {
-#pragma unroll
-            for (int d = 0; d < kPrefetch; ++d) {
-                const int s = s0 + d;
-                if (s < nsteps) {  // uniform across the workgroup
-                    const int y = ys + s * kWaves + wave;
-                    if (y < ye) store_row_lds(ring, R, y, lane, pf[d]);
-                    const int yn = y + kPrefetch * kWaves;
-                    if (yn < ye) pf[d] = load_row(f, p.W, yn, xs, lane);
-                    __syncthreads();
-                    if (y < ye) {
-                        if (temporal) compute_row_dispatch<FAM, K, true>(p, ring, R, y, xs, lane, prevf, outf);
-                        else compute_row_dispatch<FAM, K, false>(p, ring, R, y, xs, lane, prevf, outf);
-                    }
-                }
-            }
-        }
+        if (frame_temporal(p, fz))
+            ring_item<FAM, K, NCW, RPW, PD, true>(p, ring, R, pring, RP, f, frame_prev(p, fz), outf, xs, ys, ye, wave, lane);
+        else
+            ring_item<FAM, K, NCW, RPW, PD, false>(p, ring, R, pring, RP, f, nullptr, outf, xs, ys, ye, wave, lane);
     }
 }
 
@@ -279,31 +441,49 @@ __global__ __launch_bounds__(kThreads) void predict_fast(FrameSet p, int rows_pe
 template <int FAM, int K>
 static hipError_t launch_k(const FrameSet& p, hipStream_t st, int force_generic)
 {
-    const bool fast = !force_generic && p.T <= kMaxFastT && (p.W % 8) == 0 && p.W >= kHalo;
+    const bool fast = !force_generic && p.T <= kMaxFastT && (p.W % 8) == 0 && p.W >= 32;
     if (!fast) {
         size_t total = (size_t)p.W * p.H * p.nz;
         int grid = (int)std::min<size_t>((total + 255) / 256, 256 * 16);
         hipLaunchKernelGGL((predict_generic<FAM, K>), dim3(grid), dim3(256), 0, st, p);
         return hipGetLastError();
     }
-    const int R = p.T + 9;
-    const size_t lds = (size_t)R * kSlot * sizeof(uint16_t);
-    const int rows_per_seg = 128;
+    // NCW compute waves + 1 loader wave per workgroup; PD steps of NCW rows in
+    // flight.  Ring rows live during a step: y-T-1 .. y+NCW-1 plus the PD
+    // steps being loaded: R >= NCW*(PD+1) + T + 1.
+    const bool any_temporal = p.video && (p.nz > 1 || (p.z0 & 1));
+    // tiles formulas are the heaviest: two rows per compute wave per step
+    // amortise the step barrier (measured: tiles P4 0.28 -> 0.25 ms, angle
+    // and space best with one row per wave and a deeper prefetch)
+    constexpr int NCW = 4;
+    constexpr int RPW = FAM == 0 ? 2 : 1;
+    constexpr int PD = FAM == 0 ? 2 : 3;
+    const void* fn = (const void*)predict_ring<FAM, K, NCW, RPW, PD>;
+    const int R = NCW * RPW * (PD + 1) + p.T + 1;
+    const int RP = any_temporal ? NCW * RPW * (PD + 1) : 0;
+    const int halo = p.T <= 15 ? 16 : 32;
+    const size_t lds = ((size_t)R * (halo + kStrip) + (size_t)RP * kStrip) * sizeof(uint16_t);
+    static const int seg_env = getenv("LFM_SEGROWS") ? atoi(getenv("LFM_SEGROWS")) : 0;
+    const int rows_per_seg = seg_env > 0 ? seg_env : 256;
     const int nseg = (p.H + rows_per_seg - 1) / rows_per_seg;
     const int nstrip = (p.W + kStrip - 1) / kStrip;
     const int items = p.nz * nseg * nstrip;
     int occ = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)predict_fast<FAM, K>, kThreads, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NCW * 64 + 64, lds);
     if (e != hipSuccess || occ <= 0) occ = 1;
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
     const int resident = occ * ncu;
-    // equal item counts per workgroup where possible
     const int rounds = (items + resident - 1) / resident;
     const int grid = std::max(1, (items + rounds - 1) / rounds);
-    hipLaunchKernelGGL((predict_fast<FAM, K>), dim3(grid), dim3(kThreads), lds, st, p, rows_per_seg, nseg, nstrip);
+    FrameSet pp = p;
+    pp.halo = halo;
+    int a_rows = rows_per_seg, a_nseg = nseg, a_nstrip = nstrip, a_R = R, a_RP = RP;
+    void* args[] = {(void*)&pp, (void*)&a_rows, (void*)&a_nseg, (void*)&a_nstrip, (void*)&a_R, (void*)&a_RP};
+    e = hipLaunchKernel(fn, dim3(grid), dim3(NCW * 64 + 64), args, lds, st);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -336,7 +516,7 @@ extern "C" int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uin
         return hipMemcpyAsync(d_out, d_in, bytes, hipMemcpyDeviceToDevice, stream) == hipSuccess ? LFM_HIP_OK
                                                                                                    : LFM_HIP_ERUNTIME;
     }
-    lfm::FrameSet p{d_in, d_prev, d_out, W, H, T, nframes, z0, video_bit & 1};
+    lfm::FrameSet p{d_in, d_prev, d_out, W, H, T, nframes, z0, video_bit & 1, 0};
     if ((video_bit & 1) && ((z0 & 1) != 0) && d_prev == nullptr) return LFM_HIP_EINVAL;
     const int force_generic = lfm_hip_force_generic();
     hipError_t e = hipErrorInvalidValue;

@@ -388,13 +388,32 @@ float lfmo_entropy_chunk(const uint8_t* c, uint32_t S, uint32_t* hist /* 65536 s
     memset(hist, 0, 65536 * sizeof(uint32_t));
     for (uint32_t j = 0; j < S; ++j) hist[((uint32_t)L[j] << 8) | L[j + 1]]++;
     free(L);
-    float e = 0.0f;
+    /* sum_bwt_GPU reduces the 65535 terms with thrust::reduce, whose order is
+     * not pinned by the reference.  The oracle uses the fixed order of the
+     * HIP kernel (ent_sum): 256 sequential partial sums of 256 bins, a 64-lane
+     * xor-butterfly per wave, then the 4 wave sums left to right. */
     const float fs = (float)S;
-    for (uint32_t b = 0; b < 65535; ++b) {
-        if (!hist[b]) continue;
-        float P = (float)hist[b] / fs;
-        e += -1 * P * logf(P);
+    float part[256];
+    for (int t = 0; t < 256; ++t) {
+        float e = 0.0f;
+        for (uint32_t b = (uint32_t)t * 256; b < (uint32_t)t * 256 + 256 && b < 65535; ++b) {
+            if (!hist[b]) continue;
+            float P = (float)hist[b] / fs;
+            e += -1 * P * logf(P);
+        }
+        part[t] = e;
     }
+    float w[4];
+    for (int wv = 0; wv < 4; ++wv) {
+        float v[64], nv[64];
+        for (int l = 0; l < 64; ++l) v[l] = part[wv * 64 + l];
+        for (int off = 32; off > 0; off >>= 1) {
+            for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+            memcpy(v, nv, sizeof(v));
+        }
+        w[wv] = v[0];
+    }
+    float e = ((w[0] + w[1]) + w[2]) + w[3];
     return e;
 }
 
