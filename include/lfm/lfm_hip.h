@@ -43,6 +43,11 @@ enum lfm_hip_status {
 int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uint16_t* d_out, int W, int H, int nframes,
                     int T, int family, int predictor, int video_bit, int z0, void* stream);
 
+/* The seven spatial candidates of one frame (predictors 1..7, symbolized) in
+ * one launch: candidate k goes to d_out7 + (k-1)*W*H. */
+int lfm_hip_predict_candidates(const uint16_t* d_frame, uint16_t* d_out7, int W, int H, int T, int family,
+                               void* stream);
+
 /* 2D entropy of a candidate buffer of npix uint16 symbols (450000-pixel
  * chunks, klb_imageIO.cpp:2030-2093).  Synchronous: writes the float result
  * (without the 0.96 raw-candidate factor) to *entropy. */

@@ -17,11 +17,12 @@
 //             offsets
 //   scatter : stable counting sort, one wave per segment; in-wave stable rank
 //             from eight 64-bit ballots (peer mask), running counts in LDS
-//   bigram  : per <= 61440 pairs, 65536 16-bit counters packed in 128 KiB LDS
-//             (cannot overflow), run-length pre-aggregation per lane, flush of
-//             non-zero bins with global atomics
-//   entropy : per job, -P logf P over 65535 bins, fixed-order wave-shuffle
-//             reduction (deterministic)
+//   bigram  : per 30720-pair slice, staged in LDS, 65536 16-bit counters
+//             packed in 128 KiB LDS (cannot overflow), run-length
+//             pre-aggregation per thread, non-zero bins added to the job's
+//             histogram with global atomics
+//   entropy : per job, -P logf P per bin in parallel, then fixed-order row
+//             sums and wave butterflies (deterministic)
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
@@ -34,8 +35,6 @@ constexpr uint32_t kChunkPix = 450000;
 constexpr uint32_t kChunkBytes = 2 * kChunkPix;
 constexpr uint32_t kSeg = 4096;                                   // bytes per count/scatter segment
 constexpr uint32_t kSegMax = (kChunkBytes + kSeg - 1) / kSeg;     // 220
-constexpr uint32_t kPairsPerWG = 61440;                           // <= 65535 keeps 16-bit counters exact
-constexpr uint32_t kBins = 65536;
 constexpr uint32_t kLStride = (kChunkBytes + 1 + 255) & ~255u;
 
 struct Jobs {
@@ -55,6 +54,7 @@ __device__ __forceinline__ void job_span(const Jobs& J, int job, const uint8_t*&
 }
 
 // ---------------------------------------------------------------- count --
+// one 4 KiB segment per workgroup, 16 bytes per thread from one 16-byte load
 __global__ __launch_bounds__(256) void ent_count(Jobs J, uint32_t* __restrict__ cnt)
 {
     __shared__ uint32_t h[256];
@@ -65,16 +65,24 @@ __global__ __launch_bounds__(256) void ent_count(Jobs J, uint32_t* __restrict__ 
     const uint32_t s0 = blockIdx.x * kSeg;
     h[threadIdx.x] = 0;
     __syncthreads();
-    if (s0 < S) {
-        const uint32_t e = min(S, s0 + kSeg);
+    const uint32_t i = s0 + threadIdx.x * 16;
+    if (i < S) {
+        uint32_t w[4];
+        const uint32_t m = min(16u, S - i);
+        if (m == 16) {
+            const uint4 v = *(const uint4*)(c + i);  // chunk starts are 16-byte aligned (450000 px * 2 B)
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+            for (int q = 0; q < 4; ++q) w[q] = 0;
+            for (uint32_t t = 0; t < m; ++t) w[t >> 2] |= (uint32_t)c[i + t] << ((t & 3) * 8);
+        }
         uint32_t zeros = 0;
-        for (uint32_t i = s0 + threadIdx.x * 16; i < e; i += 256 * 16) {
-            const uint32_t m = min(16u, e - i);
-            for (uint32_t t = 0; t < m; ++t) {
-                const uint8_t b = c[i + t];
-                if (b == 0) ++zeros;
-                else atomicAdd(&h[b], 1u);
-            }
+#pragma unroll
+        for (uint32_t t = 0; t < 16; ++t) {
+            const uint32_t b = (w[t >> 2] >> ((t & 3) * 8)) & 0xFFu;
+            if (t >= m) break;
+            if (b == 0) ++zeros;
+            else atomicAdd(&h[b], 1u);
         }
         if (zeros) atomicAdd(&h[0], zeros);
     }
@@ -119,9 +127,12 @@ __global__ __launch_bounds__(256) void ent_scan(Jobs J, const uint32_t* __restri
 }
 
 // -------------------------------------------------------------- scatter --
+// One wave per 4 KiB segment.  The segment (and the byte before it) is staged
+// in LDS with 16-byte loads first, so the 64 rank rounds never wait on HBM.
 __global__ __launch_bounds__(256) void ent_scatter(Jobs J, const uint32_t* __restrict__ offs, uint8_t* __restrict__ L)
 {
     __shared__ uint32_t run[4][256];
+    __shared__ __attribute__((aligned(16))) uint8_t seg_bytes[4][kSeg + 16];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int job = blockIdx.y;
     const uint32_t seg = blockIdx.x * 4 + wave;
@@ -132,15 +143,27 @@ __global__ __launch_bounds__(256) void ent_scatter(Jobs J, const uint32_t* __res
     if (s0 >= S) return;  // whole wave leaves; no block barrier below
     const uint32_t* oj = offs + ((size_t)job * kSegMax + seg) * 256;
     for (int i = lane; i < 256; i += 64) run[wave][i] = oj[i];
+    const uint32_t e = min(S, s0 + kSeg);
+    uint8_t* sb = seg_bytes[wave] + 16;  // sb[-1] = c[s0 - 1]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t o = (q * 64 + lane) * 16;
+        if (s0 + o + 16 <= e) {
+            *(uint4*)(sb + o) = *(const uint4*)(c + s0 + o);
+        } else {
+            for (uint32_t t = 0; t < 16; ++t) sb[o + t] = s0 + o + t < e ? c[s0 + o + t] : 0;
+        }
+    }
+    if (lane == 0) sb[-1] = s0 > 0 ? c[s0 - 1] : 0;
+    __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
     uint8_t* Lj = L + (size_t)job * kLStride;
-    const uint32_t e = min(S, s0 + kSeg);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t g = s0; g < e; g += 64) {
+    for (uint32_t g = 0; g < e - s0; g += 64) {
         const uint32_t i = g + lane;
-        const bool valid = i < e;
-        const uint32_t key = valid ? c[i] : 0u;
-        const uint32_t val = (valid && i > 0) ? c[i - 1] : 0u;
+        const bool valid = s0 + i < e;
+        const uint32_t key = valid ? sb[i] : 0u;
+        const uint32_t val = valid ? sb[(int)i - 1] : 0u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -161,39 +184,56 @@ __global__ __launch_bounds__(256) void ent_scatter(Jobs J, const uint32_t* __res
 }
 
 // --------------------------------------------------------------- bigram --
-__global__ __launch_bounds__(256) void ent_bigram(Jobs J, const uint8_t* __restrict__ L, uint32_t* __restrict__ hist)
+// Workgroup (slice, job) counts the bigrams of kSlice consecutive pairs of L:
+// the slice is staged in LDS with 16-byte loads, every thread walks 60
+// consecutive pairs (run-length pre-aggregated: the long (0,0) runs of the
+// non-zero key buckets become one atomic), 65536 16-bit counters packed in
+// 128 KiB of LDS (kSlice < 65536: no overflow), then the non-zero counters are
+// added to the job's u32 histogram in HBM.
+constexpr uint32_t kBins = 65536;
+constexpr uint32_t kBigramThreads = 512;
+// 60 pairs per thread: thread ranges start 15 words apart (odd), so the byte
+// reads of a wave hit 64 distinct LDS banks; 128 KiB + 30 KiB of LDS
+constexpr uint32_t kPerThread = 60;
+constexpr uint32_t kSlice = kPerThread * kBigramThreads;
+
+__global__ __launch_bounds__(kBigramThreads) void ent_bigram(Jobs J, const uint8_t* __restrict__ L,
+                                                             uint32_t* __restrict__ hist)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t packed[];  // 32768 words = 65536 x u16
+    extern __shared__ __attribute__((aligned(16))) uint32_t packed[];  // kBins / 2 words, then the slice bytes
+    uint8_t* sl = (uint8_t*)(packed + kBins / 2);
     const int job = blockIdx.y;
     const uint8_t* c;
     uint32_t S;
     job_span(J, job, c, S);
-    const uint32_t p0 = blockIdx.x * kPairsPerWG;
+    const uint32_t p0 = blockIdx.x * kSlice;
     if (p0 >= S) return;  // uniform for the block
-    for (uint32_t w = threadIdx.x; w < kBins / 2; w += 256) packed[w] = 0;
-    __syncthreads();
+    const uint32_t n = min(kSlice, S - p0);  // pairs p0 .. p0+n-1 use L[p0 .. p0+n]
     const uint8_t* Lj = L + (size_t)job * kLStride;
-    const uint32_t p1 = min(S, p0 + kPairsPerWG);
-    const uint32_t per = (kPairsPerWG + 255) / 256;
-    const uint32_t a0 = p0 + threadIdx.x * per;
-    const uint32_t a1 = min(p1, a0 + per);
-    uint32_t cur = 0xFFFFFFFFu, n = 0;
+    // L job stride and p0 are multiples of 16: the staged span is 16-byte aligned
+    for (uint32_t o = threadIdx.x * 16; o < n + 1; o += kBigramThreads * 16)
+        *(uint4*)(sl + o) = *(const uint4*)(Lj + p0 + o);  // reads stay inside the L stride's slack
+    for (uint32_t w = threadIdx.x; w < kBins / 2; w += kBigramThreads) packed[w] = 0;
+    __syncthreads();
+    const uint32_t a0 = threadIdx.x * kPerThread;
+    const uint32_t a1 = min(n, a0 + kPerThread);
+    uint32_t cur = 0xFFFFFFFFu, cnt = 0;
     if (a0 < a1) {
-        uint32_t prev = Lj[a0];
+        uint32_t prev = sl[a0];
         for (uint32_t j = a0; j < a1; ++j) {
-            const uint32_t nxt = Lj[j + 1];
+            const uint32_t nxt = sl[j + 1];
             const uint32_t bin = (prev << 8) | nxt;
             prev = nxt;
-            if (bin == cur) { ++n; continue; }
-            if (n) atomicAdd(&packed[cur >> 1], n << ((cur & 1) * 16));
+            if (bin == cur) { ++cnt; continue; }
+            if (cnt) atomicAdd(&packed[cur >> 1], cnt << ((cur & 1) * 16));
             cur = bin;
-            n = 1;
+            cnt = 1;
         }
-        if (n) atomicAdd(&packed[cur >> 1], n << ((cur & 1) * 16));
+        if (cnt) atomicAdd(&packed[cur >> 1], cnt << ((cur & 1) * 16));
     }
     __syncthreads();
     uint32_t* hj = hist + (size_t)job * kBins;
-    for (uint32_t w = threadIdx.x; w < kBins / 2; w += 256) {
+    for (uint32_t w = threadIdx.x; w < kBins / 2; w += kBigramThreads) {
         const uint32_t v = packed[w];
         if (v & 0xFFFFu) atomicAdd(&hj[2 * w], v & 0xFFFFu);
         if (v >> 16) atomicAdd(&hj[2 * w + 1], v >> 16);
@@ -201,29 +241,45 @@ __global__ __launch_bounds__(256) void ent_bigram(Jobs J, const uint8_t* __restr
 }
 
 // -------------------------------------------------------------- entropy --
+// Per job: H = sum over bins b < 65535 of -P logf P, P = h / S, in the fixed
+// order the oracle restates (lfm_oracle.c lfmo_entropy_chunk): row r (bins
+// 256r .. 256r+255) summed in ascending order by one lane, the 64 rows of a
+// quarter combined by the wave's xor butterfly, quarters ((q0+q1)+q2)+q3.
+// The per-bin terms are formed by all threads into LDS first (they do not
+// depend on the order), then one wave runs the ordered row sums.
+constexpr int kRow = 257;
 __global__ __launch_bounds__(256) void ent_sum(Jobs J, const uint32_t* __restrict__ hist, float* __restrict__ ent)
 {
-    __shared__ float part[4];
+    extern __shared__ float term[];  // 64 rows x kRow
+    __shared__ float quarter[4];
     const int job = blockIdx.x;
     const uint8_t* c;
     uint32_t S;
     job_span(J, job, c, S);
     const float fs = (float)S;
     const uint32_t* hj = hist + (size_t)job * kBins;
-    float e = 0.f;
-    const uint32_t b0 = threadIdx.x * 256;
-    for (uint32_t b = b0; b < b0 + 256; ++b) {
-        if (b >= 65535u) break;  // bin 0xFFFF is never summed by the reference
-        const uint32_t h = hj[b];
-        if (h) {
-            const float P = (float)h / fs;
-            e += -1.0f * P * logf(P);
+    for (int q = 0; q < 4; ++q) {
+        for (uint32_t i = threadIdx.x; i < 16384; i += 256) {
+            const uint32_t b = q * 16384 + i;
+            const uint32_t h = hj[b];
+            float t = 0.f;
+            if (h && b != 0xFFFFu) {  // bin 0xFFFF is never summed by the reference
+                const float P = (float)h / fs;
+                t = -1.0f * P * logf(P);
+            }
+            term[(i >> 8) * kRow + (i & 255)] = t;
         }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const float* row = term + threadIdx.x * kRow;
+            float e = 0.f;
+            for (int k = 0; k < 256; ++k) e += row[k];
+            for (int off = 32; off > 0; off >>= 1) e += __shfl_xor(e, off);
+            if (threadIdx.x == 0) quarter[q] = e;
+        }
+        __syncthreads();
     }
-    for (int off = 32; off > 0; off >>= 1) e += __shfl_xor(e, off);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = e;
-    __syncthreads();
-    if (threadIdx.x == 0) ent[job] = ((part[0] + part[1]) + part[2]) + part[3];
+    if (threadIdx.x == 0) ent[job] = ((quarter[0] + quarter[1]) + quarter[2]) + quarter[3];
 }
 
 struct Workspace {
@@ -256,15 +312,15 @@ static size_t workspace_layout(uint64_t npix, int ncand, bool with_cands, Worksp
 static hipError_t run_entropy(const Jobs& J, const Workspace& w, hipStream_t st)
 {
     const uint32_t nsegBlocks = kSegMax;
-    hipError_t e;
-    e = hipMemsetAsync(w.hist, 0, (size_t)J.njobs * kBins * 4, st);
+    hipError_t e = hipMemsetAsync(w.hist, 0, (size_t)J.njobs * kBins * 4, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ent_count, dim3(nsegBlocks, J.njobs), dim3(256), 0, st, J, w.cnt);
     hipLaunchKernelGGL(ent_scan, dim3(J.njobs), dim3(256), 0, st, J, w.cnt, w.offs, w.L);
     hipLaunchKernelGGL(ent_scatter, dim3((nsegBlocks + 3) / 4, J.njobs), dim3(256), 0, st, J, w.offs, w.L);
-    const uint32_t nbig = (kChunkBytes + kPairsPerWG - 1) / kPairsPerWG;
-    hipLaunchKernelGGL(ent_bigram, dim3(nbig, J.njobs), dim3(256), (kBins / 2) * 4, st, J, w.L, w.hist);
-    hipLaunchKernelGGL(ent_sum, dim3(J.njobs), dim3(256), 0, st, J, w.hist, w.ent);
+    const uint32_t nslice = (kChunkBytes + kSlice - 1) / kSlice;
+    hipLaunchKernelGGL(ent_bigram, dim3(nslice, J.njobs), dim3(kBigramThreads), (kBins / 2) * 4 + kSlice + 16, st, J,
+                       w.L, w.hist);
+    hipLaunchKernelGGL(ent_sum, dim3(J.njobs), dim3(256), 64 * kRow * 4, st, J, w.hist, w.ent);
     return hipGetLastError();
 }
 
@@ -333,12 +389,8 @@ extern "C" int lfm_hip_select(const uint16_t* d_frame, int W, int H, int T, int 
     workspace_layout(npix, 8, true, &w, (uint8_t*)ws);
     const uint16_t* cands[8];
     cands[0] = d_frame;  // candidate 0: the raw frame (klb_imageIO.cpp:1690)
-    int rc = LFM_HIP_OK;
-    for (int k = 1; k < 8 && rc == LFM_HIP_OK; ++k) {
-        uint16_t* dst = w.cands + (size_t)(k - 1) * npix;
-        rc = lfm_hip_predict(d_frame, nullptr, dst, W, H, 1, T, family, k, 0, 0, st);
-        cands[k] = dst;
-    }
+    for (int k = 1; k < 8; ++k) cands[k] = w.cands + (size_t)(k - 1) * npix;
+    int rc = lfm_hip_predict_candidates(d_frame, w.cands, W, H, T, family, st);
     float ent[8];
     if (rc == LFM_HIP_OK) rc = entropy_impl(cands, 8, npix, ent, ws, false, st);
     if (own) (void)hipFreeAsync(ws, st);

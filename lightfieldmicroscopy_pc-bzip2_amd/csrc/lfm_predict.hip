@@ -6,20 +6,23 @@
 // host<->device copies of Predictor_both (klb_imageIO.cpp:1244-1313).
 //
 // Fast kernel layout (W % 8 == 0, Nnum <= 31):
-//   * one workgroup = 4 waves owns a 512-pixel-wide strip of a frame and
-//     marches down a segment of rows; the input rows stream HBM -> VGPR
-//     (16 B per lane, prefetched two steps ahead) -> an LDS ring of T+9 row
-//     slots (32-pixel left halo + 512 pixels);
-//   * each step every wave computes one row: lane l handles columns
-//     l, l+64, ..., l+448 so every LDS neighbour read is conflict-free;
+//   * one workgroup = NCW compute waves + 1 loader wave owns a 512-pixel strip
+//     of one frame and marches down a piece of its rows;
+//   * the loader wave streams rows HBM -> LDS with LDS-DMA
+//     (global_load_lds_dwordx4: 16 B per lane, one instruction per 512-pixel
+//     row + one for the left halo) PD steps ahead into a ring of
+//     NCW*RPW*(PD+1)+T+1 row slots (halo + 512 pixels), counting its own
+//     vmcnt so compute waves never wait on memory they do not need;
+//   * each step every compute wave computes RPW rows: lane l handles columns
+//     l, l+64, ..., l+448, so every LDS neighbour read is conflict-free;
 //   * residual -> int16 -> symbol in registers, one 2-byte store per pixel
 //     (128 contiguous bytes per wave instruction);
-//   * all frames of a stack in one launch, workgroups grid-stride over
-//     (frame, row segment, strip) work items.
-// Every input pixel is read from HBM once (+ the 32-pixel halo per strip and
-// the T+1 primed rows per segment, served mostly from L2 / MALL); every symbol
-// is written once.  Algorithmic traffic: 2 B read + 2 B written per pixel,
-// +2 B read on temporal frames.
+//   * all frames of a stack in one launch; the launcher splits frames into
+//     row pieces so the (frame, piece, strip) items fill the GPU about once.
+// Every input pixel is read from HBM once (+ the 16/32-pixel halo per strip
+// row, an L2 hit under the XCD-aware mapping, and the T+1 primed rows per
+// piece); every symbol is written once.  Algorithmic traffic: 2 B read + 2 B
+// written per pixel, +2 B read on temporal frames.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
@@ -27,6 +30,10 @@
 #include "lfm_hip.h"
 
 namespace lfm {
+
+// Symbols are written once and not re-read by this launch: non-temporal
+// stores (measured 1-3 % faster than plain stores; nt loads were 3 % slower).
+__device__ __forceinline__ void store_sym(uint16_t* p, uint16_t v) { __builtin_nontemporal_store(v, p); }
 
 constexpr int kStrip = 512;           // pixels per strip (64 lanes x 8)
 // LDS row slot = left halo + 512 strip pixels; the halo covers x - T - 1:
@@ -189,7 +196,7 @@ __device__ __forceinline__ void slow_row(const RowPtrs& r, int y, int xs, int W,
         const int I = r.q0[j * 64];
         const int P = TEMP ? (int)prow[j * 64] : 0;
         const int res = residual_any_case<FAM, K, TEMP>(g, tile_case(tx, ty), pos_case(u, v), I, P);
-        orow[j * 64] = (uint16_t)symbolize16(res);
+        store_sym(orow + j * 64, (uint16_t)symbolize16(res));
     }
 }
 
@@ -205,7 +212,7 @@ __device__ __forceinline__ void fast_px(const RowPtrs& r, uint32_t u0bits, int l
     const int I = r.q0[J * 64];
     const int P = TEMP ? (int)prow[J * 64] : 0;
     if constexpr (K == 0) {  // diagnostic ablation: same loads / LDS / stores, no prediction
-        orow[J * 64] = (uint16_t)(I + P);
+        store_sym(orow + J * 64, (uint16_t)(I + P));
         return;
     }
     // both candidates are evaluated and blended with a mask: no divergent branch
@@ -220,7 +227,7 @@ __device__ __forceinline__ void fast_px(const RowPtrs& r, uint32_t u0bits, int l
         const int rt = t_i ^ ((t_u ^ t_i) & m0);
         res = res ^ ((rt ^ res) & mt);
     }
-    orow[J * 64] = (uint16_t)symbolize16(res);
+    store_sym(orow + J * 64, (uint16_t)symbolize16(res));
 }
 
 template <int FAM, int K, bool TEMP, bool V0, bool FIRST>
@@ -381,7 +388,7 @@ __device__ __forceinline__ void ring_item(const FrameSet& p, uint16_t* ring, int
     }
     for (int s = 0; s < nsteps; ++s) {
         if (loader) {
-            if (s + PD < nsteps) wait_vmcnt<kLoadsPerStep * (PD - 1)>();
+            if (s + PD < nsteps) wait_vmcnt<(kLoadsPerStep * (PD - 1) < 63 ? kLoadsPerStep * (PD - 1) : 63)>();
             else wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
@@ -410,9 +417,14 @@ __device__ __forceinline__ void ring_item(const FrameSet& p, uint16_t* ring, int
     __builtin_amdgcn_s_barrier();
 }
 
+// One workgroup per item (frame, row piece, strip).  With xcd_map the nstrip
+// workgroups of one (frame, piece) are blockIdx b, b+8, b+16, ... which the
+// dispatcher deals to one XCD: the 32-byte left halo of a strip row is then
+// an L2 hit on the row its neighbour strip streamed a few microseconds
+// earlier instead of a second HBM fetch of that 128-byte line.
 template <int FAM, int K, int NCW, int RPW, int PD>
-__global__ __launch_bounds__(NCW * 64 + 64) void predict_ring(FrameSet p, int rows_per_seg, int nseg, int nstrip,
-                                                              int R, int RP)
+__global__ __launch_bounds__(NCW * 64 + 64) void predict_ring(FrameSet p, int rows_per_piece, int npiece, int nstrip,
+                                                              int xcd_map, int R, int RP)
 {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
     uint16_t* ring = lds;
@@ -420,71 +432,161 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_ring(FrameSet p, int ro
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const size_t fs = (size_t)p.W * p.H;
-    const int items = p.nz * nseg * nstrip;
-    for (int item = blockIdx.x; item < items; item += gridDim.x) {
-        const int strip = item % nstrip;
-        const int seg = (item / nstrip) % nseg;
-        const int fz = item / (nstrip * nseg);
-        const int xs = strip * kStrip;
-        const int ys = seg * rows_per_seg;
-        const int ye = min(ys + rows_per_seg, p.H);
-        const uint16_t* f = p.in + (size_t)fz * fs;
-        uint16_t* outf = p.out + (size_t)fz * fs;
-        if (frame_temporal(p, fz))
-            ring_item<FAM, K, NCW, RPW, PD, true>(p, ring, R, pring, RP, f, frame_prev(p, fz), outf, xs, ys, ye, wave, lane);
-        else
-            ring_item<FAM, K, NCW, RPW, PD, false>(p, ring, R, pring, RP, f, nullptr, outf, xs, ys, ye, wave, lane);
+    const int b = blockIdx.x;
+    int strip, group;
+    if (xcd_map) {
+        const int q = b >> 3;
+        strip = q % nstrip;
+        group = (q / nstrip) * 8 + (b & 7);
+    } else {
+        strip = b % nstrip;
+        group = b / nstrip;
+    }
+    const int piece = group % npiece;
+    const int fz = group / npiece;
+    if (fz >= p.nz) return;
+    const int xs = strip * kStrip;
+    const int ys = piece * rows_per_piece;
+    const int ye = min(ys + rows_per_piece, p.H);
+    if (ys >= ye) return;
+    const uint16_t* f = p.in + (size_t)fz * fs;
+    uint16_t* outf = p.out + (size_t)fz * fs;
+    if (frame_temporal(p, fz))
+        ring_item<FAM, K, NCW, RPW, PD, true>(p, ring, R, pring, RP, f, frame_prev(p, fz), outf, xs, ys, ye, wave, lane);
+    else
+        ring_item<FAM, K, NCW, RPW, PD, false>(p, ring, R, pring, RP, f, nullptr, outf, xs, ys, ye, wave, lane);
+}
+
+// All seven spatial candidates of one frame in one launch (selection pass,
+// klb_imageIO.cpp:1671-1746 runs them as seven serial launch sequences):
+// blockIdx.y = k - 1 writes candidate k to out + (k - 1) * W * H.
+template <int FAM, int NCW, int RPW, int PD>
+__global__ __launch_bounds__(NCW * 64 + 64) void predict_cands(FrameSet p, int rows_per_piece, int npiece, int nstrip,
+                                                               int xcd_map, int R, int RP)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int b = blockIdx.x;
+    int strip, piece;
+    if (xcd_map) {
+        const int q = b >> 3;
+        strip = q % nstrip;
+        piece = (q / nstrip) * 8 + (b & 7);
+    } else {
+        strip = b % nstrip;
+        piece = b / nstrip;
+    }
+    const int xs = strip * kStrip;
+    const int ys = piece * rows_per_piece;
+    const int ye = min(ys + rows_per_piece, p.H);
+    if (ys >= ye) return;
+    uint16_t* outf = p.out + (size_t)blockIdx.y * p.W * p.H;
+    switch (blockIdx.y) {
+#define LFM_CAND(KK)                                                                                                  \
+    case KK - 1:                                                                                                      \
+        ring_item<FAM, KK, NCW, RPW, PD, false>(p, lds, R, nullptr, RP, p.in, nullptr, outf, xs, ys, ye, wave, lane); \
+        break;
+        LFM_CAND(1) LFM_CAND(2) LFM_CAND(3) LFM_CAND(4) LFM_CAND(5) LFM_CAND(6) LFM_CAND(7)
+#undef LFM_CAND
     }
 }
 
 // -------------------------------------------------------------- launchers --
-template <int FAM, int K>
-static hipError_t launch_k(const FrameSet& p, hipStream_t st, int force_generic)
+// NCW compute waves + 1 loader wave per workgroup; PD steps of NCW*RPW rows in
+// flight.  Ring rows live during a step: y-T-1 .. y+NCW*RPW-1 plus the PD
+// steps being loaded: R >= NCW*RPW*(PD+1) + T + 1.
+// tiles formulas are the heaviest: two rows per compute wave per step
+// amortise the step barrier (tiles P4 0.28 -> 0.25 ms); angle / space run
+// best with one row per wave and 3 steps of prefetch (deeper prefetch costs a
+// workgroup of occupancy per CU and measured 5-8 % slower).
+template <int FAM>
+struct RingShape {
+    static constexpr int NCW = 4;
+    static constexpr int RPW = FAM == 0 ? 2 : 1;
+    static constexpr int PD = FAM == 0 ? 2 : 3;
+};
+
+struct Plan {
+    int R, RP, halo, rows_per_piece, npiece, nstrip, xcd_map, grid;
+    size_t lds;
+};
+
+// Split each frame into npiece row pieces so that the items (copies x frames
+// x pieces x strips) fill the resident workgroup slots about once: a piece
+// re-reads only its T+1 priming rows, so fewer, taller pieces waste less
+// (1.5 % at 2048 rows / 3 pieces vs 6 % for 256-row segments).  Pieces stay
+// >= 2(T+1) rows.
+static hipError_t make_plan(const FrameSet& p, const void* fn, int ncw, int rpw, int pd, int copies, Plan& pl)
 {
-    const bool fast = !force_generic && p.T <= kMaxFastT && (p.W % 8) == 0 && p.W >= 32;
-    if (!fast) {
-        size_t total = (size_t)p.W * p.H * p.nz;
-        int grid = (int)std::min<size_t>((total + 255) / 256, 256 * 16);
-        hipLaunchKernelGGL((predict_generic<FAM, K>), dim3(grid), dim3(256), 0, st, p);
-        return hipGetLastError();
-    }
-    // NCW compute waves + 1 loader wave per workgroup; PD steps of NCW rows in
-    // flight.  Ring rows live during a step: y-T-1 .. y+NCW-1 plus the PD
-    // steps being loaded: R >= NCW*(PD+1) + T + 1.
     const bool any_temporal = p.video && (p.nz > 1 || (p.z0 & 1));
-    // tiles formulas are the heaviest: two rows per compute wave per step
-    // amortise the step barrier (measured: tiles P4 0.28 -> 0.25 ms, angle
-    // and space best with one row per wave and a deeper prefetch)
-    constexpr int NCW = 4;
-    constexpr int RPW = FAM == 0 ? 2 : 1;
-    constexpr int PD = FAM == 0 ? 2 : 3;
-    const void* fn = (const void*)predict_ring<FAM, K, NCW, RPW, PD>;
-    const int R = NCW * RPW * (PD + 1) + p.T + 1;
-    const int RP = any_temporal ? NCW * RPW * (PD + 1) : 0;
-    const int halo = p.T <= 15 ? 16 : 32;
-    const size_t lds = ((size_t)R * (halo + kStrip) + (size_t)RP * kStrip) * sizeof(uint16_t);
-    static const int seg_env = getenv("LFM_SEGROWS") ? atoi(getenv("LFM_SEGROWS")) : 0;
-    const int rows_per_seg = seg_env > 0 ? seg_env : 256;
-    const int nseg = (p.H + rows_per_seg - 1) / rows_per_seg;
-    const int nstrip = (p.W + kStrip - 1) / kStrip;
-    const int items = p.nz * nseg * nstrip;
+    pl.R = ncw * rpw * (pd + 1) + p.T + 1;
+    pl.RP = any_temporal ? ncw * rpw * (pd + 1) : 0;
+    pl.halo = p.T <= 15 ? 16 : 32;
+    pl.lds = ((size_t)pl.R * (pl.halo + kStrip) + (size_t)pl.RP * kStrip) * sizeof(uint16_t);
+    pl.nstrip = (p.W + kStrip - 1) / kStrip;
     int occ = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, NCW * 64 + 64, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, ncw * 64 + 64, pl.lds);
     if (e != hipSuccess || occ <= 0) occ = 1;
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
     const int resident = occ * ncu;
-    const int rounds = (items + resident - 1) / resident;
-    const int grid = std::max(1, (items + rounds - 1) / rounds);
-    FrameSet pp = p;
-    pp.halo = halo;
-    int a_rows = rows_per_seg, a_nseg = nseg, a_nstrip = nstrip, a_R = R, a_RP = RP;
-    void* args[] = {(void*)&pp, (void*)&a_rows, (void*)&a_nseg, (void*)&a_nstrip, (void*)&a_R, (void*)&a_RP};
-    e = hipLaunchKernel(fn, dim3(grid), dim3(NCW * 64 + 64), args, lds, st);
+    const int cols = copies * p.nz * pl.nstrip;
+    int npiece = std::max(1, resident / std::max(1, cols));
+    npiece = std::min(npiece, std::max(1, p.H / (2 * (p.T + 1))));
+    int rows = (p.H + npiece - 1) / npiece;
+    rows = (rows + ncw * rpw - 1) / (ncw * rpw) * (ncw * rpw);
+    pl.rows_per_piece = rows;
+    pl.npiece = (p.H + rows - 1) / rows;
+    const int ngroups = p.nz * pl.npiece;
+    pl.xcd_map = (ngroups % 8) == 0 && pl.nstrip > 1;
+    pl.grid = ngroups * pl.nstrip;
+    return hipSuccess;
+}
+
+static hipError_t launch_plan(const void* fn, FrameSet p, const Plan& pl, int ncw, int gy, hipStream_t st)
+{
+    p.halo = pl.halo;
+    int a_rows = pl.rows_per_piece, a_np = pl.npiece, a_nstrip = pl.nstrip, a_x = pl.xcd_map, a_R = pl.R, a_RP = pl.RP;
+    void* args[] = {(void*)&p, (void*)&a_rows, (void*)&a_np, (void*)&a_nstrip, (void*)&a_x, (void*)&a_R, (void*)&a_RP};
+    hipError_t e = hipLaunchKernel(fn, dim3(pl.grid, gy), dim3(ncw * 64 + 64), args, pl.lds, st);
     if (e != hipSuccess) return e;
     return hipGetLastError();
+}
+
+static bool fast_ok(const FrameSet& p, int force_generic)
+{
+    return !force_generic && p.T <= kMaxFastT && (p.W % 8) == 0 && p.W >= 32;
+}
+
+template <int FAM, int K>
+static hipError_t launch_k(const FrameSet& p, hipStream_t st, int force_generic)
+{
+    if (!fast_ok(p, force_generic)) {
+        size_t total = (size_t)p.W * p.H * p.nz;
+        int grid = (int)std::min<size_t>((total + 255) / 256, 256 * 16);
+        hipLaunchKernelGGL((predict_generic<FAM, K>), dim3(grid), dim3(256), 0, st, p);
+        return hipGetLastError();
+    }
+    using RS = RingShape<FAM>;
+    const void* fn = (const void*)predict_ring<FAM, K, RS::NCW, RS::RPW, RS::PD>;
+    Plan pl;
+    hipError_t e = make_plan(p, fn, RS::NCW, RS::RPW, RS::PD, 1, pl);
+    if (e != hipSuccess) return e;
+    return launch_plan(fn, p, pl, RS::NCW, 1, st);
+}
+
+template <int FAM>
+static hipError_t launch_cands(const FrameSet& p, hipStream_t st)
+{
+    using RS = RingShape<FAM>;
+    const void* fn = (const void*)predict_cands<FAM, RS::NCW, RS::RPW, RS::PD>;
+    Plan pl;
+    hipError_t e = make_plan(p, fn, RS::NCW, RS::RPW, RS::PD, 7, pl);
+    if (e != hipSuccess) return e;
+    return launch_plan(fn, p, pl, RS::NCW, 7, st);
 }
 
 template <int FAM>
@@ -524,6 +626,29 @@ extern "C" int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uin
     case 0: e = lfm::launch_fam<0>(predictor, p, stream, force_generic); break;
     case 1: e = lfm::launch_fam<1>(predictor, p, stream, force_generic); break;
     case 2: e = lfm::launch_fam<2>(predictor, p, stream, force_generic); break;
+    }
+    return e == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
+}
+
+extern "C" int lfm_hip_predict_candidates(const uint16_t* d_frame, uint16_t* d_out7, int W, int H, int T, int family,
+                                          void* stream_)
+{
+    if (!d_frame || !d_out7 || W <= 0 || H <= 0 || T <= 0 || family < 0 || family > 2) return LFM_HIP_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    lfm::FrameSet p{d_frame, nullptr, d_out7, W, H, T, 1, 0, 0, 0};
+    if (!lfm::fast_ok(p, lfm_hip_force_generic())) {
+        for (int k = 1; k <= 7; ++k) {
+            const int rc = lfm_hip_predict(d_frame, nullptr, d_out7 + (size_t)(k - 1) * W * H, W, H, 1, T, family, k,
+                                           0, 0, stream_);
+            if (rc != LFM_HIP_OK) return rc;
+        }
+        return LFM_HIP_OK;
+    }
+    hipError_t e = hipErrorInvalidValue;
+    switch (family) {
+    case 0: e = lfm::launch_cands<0>(p, stream); break;
+    case 1: e = lfm::launch_cands<1>(p, stream); break;
+    case 2: e = lfm::launch_cands<2>(p, stream); break;
     }
     return e == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
 }

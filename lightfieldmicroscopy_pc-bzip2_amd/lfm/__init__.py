@@ -20,7 +20,7 @@ except Exception:  # pragma: no cover
     _HAVE_TORCH = False
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "liblfm.so")
+LIB_PATH = os.environ.get("LFM_LIB") or os.path.join(PKG_DIR, "liblfm.so")
 
 FAMILIES = {"tiles": 0, "angle_and_space": 0, "angle": 1, "space": 2}
 DTYPES = {np.dtype(np.uint8): 0, np.dtype(np.uint16): 1, np.dtype(np.uint32): 2, np.dtype(np.uint64): 3,
@@ -36,7 +36,7 @@ EXPORTS = [
     "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_decode_memory",
     # lfm_hip.h
-    "lfm_hip_predict", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
+    "lfm_hip_predict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic",
 ]
 
@@ -94,6 +94,7 @@ def lib():
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
     L.lfm_decode_memory.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_int]
     L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
+    L.lfm_hip_predict_candidates.argtypes = [vp, vp] + [ctypes.c_int] * 4 + [vp]
     L.lfm_hip_entropy2d.argtypes = [vp, ctypes.c_uint64, f32p, vp]
     L.lfm_hip_select_workspace_bytes.restype = ctypes.c_size_t
     L.lfm_hip_select_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -283,6 +284,13 @@ def predict_device(d_in, d_out, W, H, nframes, T, family, predictor, video=0, z0
     rc = lib().lfm_hip_predict(p(d_in), p(d_prev), p(d_out), W, H, nframes, T, FAMILIES.get(family, family),
                                predictor, video, z0, _stream(stream))
     _check(rc, "lfm_hip_predict")
+
+
+def predict_candidates_device(d_frame, d_out7, W, H, T, family, stream=None):
+    """The seven spatial candidates of one frame in one launch (d_out7: 7*H*W uint16)."""
+    rc = lib().lfm_hip_predict_candidates(d_frame.data_ptr(), d_out7.data_ptr(), W, H, T,
+                                          FAMILIES.get(family, family), _stream(stream))
+    _check(rc, "lfm_hip_predict_candidates")
 
 
 def select_device(d_frame, W, H, T, family, stream=None):

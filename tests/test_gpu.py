@@ -71,6 +71,21 @@ def test_fast_kernel_vs_oracle(lfmlib, oracle, gpu, W, H, T):
             assert np.array_equal(got, exp), (fam, k)
 
 
+@pytest.mark.parametrize("W,H,T", [(2048, 600, 15), (1032, 200, 13), (520, 300, 31), (45, 31, 13), (64, 40, 2)])
+def test_candidates_kernel_vs_oracle(lfmlib, oracle, gpu, W, H, T):
+    """The selection pass's one-launch seven-candidate kernel equals the oracle
+    for every predictor (fast ring shapes and the generic fallback)."""
+    torch = gpu
+    fr = oracle.synthetic_lf(W, H, Z=1, T=T, seed=W + 3 * H)[0, 0, 0]
+    d_out = torch.empty((7, H, W), dtype=torch.int16, device="cuda")
+    for fam in FAMS:
+        lfmlib.predict_candidates_device(dev16(torch, fr), d_out, W, H, T, fam)
+        torch.cuda.synchronize()
+        got = d_out.cpu().numpy().view(np.uint16)
+        for k in range(1, 8):
+            assert np.array_equal(got[k - 1], oracle.predict_frame(fr, None, T, fam, k, 0)), (fam, k)
+
+
 def test_predict_z0_offset_and_prev(lfmlib, oracle, gpu):
     """A z-slab starting at an odd z of a video stack takes its previous raw
     frame from d_prev (multi-GPU slabs use this)."""
@@ -111,6 +126,11 @@ def test_entropy_single_candidate(lfmlib, oracle, gpu):
         cand = rng.integers(0, 300, size=n, dtype=np.uint16)
         e = lfmlib.entropy_device(dev16(torch, cand))
         assert abs(e - oracle.entropy2d(cand)) <= 1e-5 * max(1.0, abs(e)), n
+    # one bin takes every pair (counts far above 16 bits), and the (0, 0) hot bin
+    for v in (0x0101, 0x0000, 0xFFFF, 0x00FF):
+        cand = np.full(900001, v, dtype=np.uint16)
+        e = lfmlib.entropy_device(dev16(torch, cand))
+        assert abs(e - oracle.entropy2d(cand)) <= 1e-5 * max(1.0, abs(e)), hex(v)
 
 
 def _manifest():
