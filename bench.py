@@ -7,9 +7,12 @@ frame 0) from HBM-resident input to a complete in-memory .lfm: GPU selection
 + one D2H copy of the symbols + bzip2 of the 96x96x8 blocks on the host cores
 + in-order assembly.  Nothing is cached between steps.
 
-Multi-GPU (torchrun, one process per GPU): every rank encodes its own stack
-(a z-slab of a larger stack; distinct data per rank), no data-path collective
-(scaling "weak"); a barrier + MAX-over-ranks of the timed region gives value.
+Multi-GPU (torchrun, one process per GPU): rank r encodes z-slab r of a
+(world x 64)-frame stack (lfm.shard: slabs are whole blocks deep, so the slab
+files join byte-identically with lfm.merge_slabs, tests/test_shard_cpu.py);
+the predictor is selected on the stack's frame 0 redundantly on every rank
+(no broadcast) and forced for the slab; no data-path collective (scaling
+"weak"); a barrier + MAX-over-ranks of the timed region gives value.
 
 Also reported: `roofline` of the dominant kernel (fused predictor, HIP-event
 time per launch on its own stream) and `cpu_baseline` = the reference's CPU
@@ -31,6 +34,7 @@ import torch  # noqa: E402  (before liblfm: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import lfm  # noqa: E402
+from lfm.shard import forced_request, max_over_ranks  # noqa: E402
 
 X, Y, Z, T = 2048, 2048, 64, 15
 FAMILY = "angle"
@@ -91,7 +95,7 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
             "sample": "%dx%dx%d uint16 synthetic slab of the bench stack, request 8 (predictor off), 96x96x8 blocks, "
                       "bzip2 level 2 (%s), %d blocks, ratio %.3f" % (X, Y, zs, bz.kind, len(blocks),
                                                                       px * 2 / total),
-            "value_1thread": px1 / dt1 / 1e6}
+            "value_1thread": px1 / dt1 / 1e6, "nproc": os.cpu_count()}
 
 
 def main():
@@ -107,9 +111,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # LFM_BENCH_BACKEND=gloo rehearses the N-rank path with several ranks on
+    # one GPU (local rank modulo the visible devices); the driver's N-GPU runs
+    # use nccl (RCCL), which only carries the barriers and the MAX reduction
+    backend = os.environ.get("LFM_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     lfm.require_gpu()
     lfm.set_family(FAMILY)
     zf = args.frames
@@ -117,12 +129,24 @@ def main():
 
     d_img = torch.empty((zf, Y, X), dtype=torch.int16, device="cuda")
     # rank r holds z-slab r of a (world * zf)-frame stack
-    lfm.synth_device(d_img, X, Y, zf, T, t_index=0, idx0=rank * zf * X * Y, seed=SEED)
+    z0 = rank * zf
+    lfm.synth_device(d_img, X, Y, zf, T, t_index=0, idx0=z0 * X * Y, seed=SEED)
+    if rank == 0:
+        d_f0 = d_img[0]
+    else:  # the stack's frame 0, for the redundant selection
+        d_f0 = torch.empty((1, Y, X), dtype=torch.int16, device="cuda")
+        lfm.synth_device(d_f0, X, Y, 1, T, t_index=0, idx0=0, seed=SEED)
     torch.cuda.synchronize()
     enc = lfm.Encoder(device=local, num_threads=threads)
 
     def step():
-        return enc.encode(d_img, header_version=0, nnum=T)
+        t0 = time.perf_counter()
+        k, _ = lfm.select_device(d_f0, X, Y, T, FAMILY)  # selection on the stack's frame 0
+        sel_ms = (time.perf_counter() - t0) * 1e3
+        b, st = enc.encode_slab(d_img, z0, header_version=forced_request(k), nnum=T)
+        st["select_ms"] = sel_ms
+        st["total_ms"] += sel_ms
+        return b, st
 
     for _ in range(args.warmup):
         step()
@@ -139,11 +163,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     px_rank = X * Y * zf
     value = world * px_rank * args.steps / elapsed / 1e6
@@ -151,11 +171,11 @@ def main():
     alg_bytes = px_rank * 4  # 2 B read + 2 B written per pixel (no temporal frames in this config)
     achieved = alg_bytes / (pred_ms / 1e3) / 1e9
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic_predict_fast.json")
+    tpath = os.path.join(REPO, "profiles", "r01_traffic_predict.json")
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-        except Exception:
+        except (OSError, ValueError):
             traffic = None
     line = {
         "metric": "uint16 Mpixel/s encode (predictor->bzip2) at 1/2/4/8 GPUs; ratio parity",
@@ -175,8 +195,10 @@ def main():
                    "parallelism": "z-slab per GPU (no collective)", "host_threads_per_gpu": threads},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                     "kernel": "lfm::predict_fast<1,K> (fused predictor+symbolize, %d frames per launch)" % zf,
-                     "kernel_ms": round(pred_ms, 4), "algorithmic_bytes": alg_bytes},
+                     "kernel": "lfm::predict_ring<1,K,4,1,3> (fused angle predictor + symbolize, %d frames per "
+                               "launch)" % zf,
+                     "kernel_ms": round(pred_ms, 4), "algorithmic_bytes": alg_bytes,
+                     "read_only_frac": round(px_rank * 2 / (pred_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
         "stages_ms": {k: round(float(np.mean([s[k] for s in stats])), 3)
                       for k in ("select_ms", "predict_ms", "d2h_ms", "compress_ms", "total_ms")},
         "chosen_predictor": stats[-1]["chosen"],

@@ -66,6 +66,27 @@ LFM_API int lfm_encoder_encode(lfm_encoder* enc, const void* img, int img_is_dev
                                const char metadata[KLB_METADATA_SIZE], const uint8_t** out, uint64_t* out_len,
                                lfm_encode_stats* stats);
 
+/* Encode z-slab [z0, z0 + xyzct[2]) of a larger stack (c = t = 1) for
+ * multi-GPU sharding: frame z of the slab is temporal when video & (z0 + z)
+ * is odd, and the slab's first frame then uses prev_frame (the raw frame
+ * z0 - 1, host or device like img).  Use a forced predictor request (8 + k,
+ * k selected on the whole stack's frame 0) so every slab codes like the
+ * whole stack would; slab depths must be multiples of the block depth except
+ * the last.  The result is a valid .lfm of the slab (lfm_merge_slabs joins
+ * them). */
+LFM_API int lfm_encoder_encode_slab(lfm_encoder* enc, const void* img, int img_is_device, const void* prev_frame,
+                                    uint32_t z0, const uint32_t xyzct[KLB_DATA_DIMS], int dataType,
+                                    int headerVersion, int Nnum, const uint32_t blockSize[KLB_DATA_DIMS],
+                                    int compressionType, const char metadata[KLB_METADATA_SIZE],
+                                    const uint8_t** out, uint64_t* out_len, lfm_encode_stats* stats);
+
+/* Join the .lfm files of consecutive z-slabs into the whole stack's .lfm
+ * (byte-identical to encoding the stack in one piece).  *out is malloc'ed:
+ * release it with lfm_free.  Returns 0, or 3 when the slabs do not fit. */
+LFM_API int lfm_merge_slabs(const uint8_t* const* slabs, const uint64_t* lens, int nslabs, uint8_t** out,
+                            uint64_t* out_len);
+LFM_API void lfm_free(void* p);
+
 /* Decode an in-memory .lfm into `img` (host, getImageSizeBytes bytes). */
 LFM_API int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads);
 

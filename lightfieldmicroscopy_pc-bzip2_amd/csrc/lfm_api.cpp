@@ -1,5 +1,6 @@
 // lfm_api.cpp -- liblfm extensions (lfm_api.h).
 #include "lfm_api.h"
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include "klb_imageIO.h"
@@ -68,6 +69,44 @@ extern "C" int lfm_encoder_encode(lfm_encoder* e, const void* img, int img_is_de
     *out_len = e->enc.mem_out.size();
     return rc;
 }
+
+extern "C" int lfm_encoder_encode_slab(lfm_encoder* e, const void* img, int img_is_device, const void* prev_frame,
+                                       uint32_t z0, const uint32_t xyzct[KLB_DATA_DIMS], int dataType,
+                                       int headerVersion, int Nnum, const uint32_t blockSize[KLB_DATA_DIMS],
+                                       int compressionType, const char metadata[KLB_METADATA_SIZE],
+                                       const uint8_t** out, uint64_t* out_len, lfm_encode_stats* stats)
+{
+    if (!e || !img || !out || !out_len) return 3;
+    klb_image_header h;
+    h.setHeader(xyzct, (KLB_DATA_TYPE)dataType, nullptr, blockSize, (KLB_COMPRESSION_TYPE)compressionType, metadata,
+                (uint8_t)headerVersion, (uint8_t)Nnum);
+    lfm::SlabSpec slab;
+    slab.z0 = z0;
+    slab.prev = prev_frame;
+    lfm::MemSink sink(&e->enc.mem_out);
+    int rc = e->enc.encode(img, img_is_device != 0, h, sink, stats, e->threads, &slab);
+    *out = e->enc.mem_out.data();
+    *out_len = e->enc.mem_out.size();
+    return rc;
+}
+
+extern "C" int lfm_merge_slabs(const uint8_t* const* slabs, const uint64_t* lens, int nslabs, uint8_t** out,
+                               uint64_t* out_len)
+{
+    if (!out || !out_len) return 3;
+    *out = nullptr;
+    *out_len = 0;
+    std::vector<uint8_t> v;
+    int rc = lfm::merge_slabs(slabs, lens, nslabs, &v);
+    if (rc) return rc;
+    *out = (uint8_t*)std::malloc(v.size() ? v.size() : 1);
+    if (!*out) return 3;
+    std::memcpy(*out, v.data(), v.size());
+    *out_len = v.size();
+    return 0;
+}
+
+extern "C" void lfm_free(void* p) { std::free(p); }
 
 extern "C" int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads)
 {

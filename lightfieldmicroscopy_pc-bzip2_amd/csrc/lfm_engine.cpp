@@ -338,7 +338,7 @@ void* Encoder::dev_alloc(void*& p, size_t& cap, size_t need)
 }
 
 int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym,
-                             lfm_encode_stats* st)
+                             lfm_encode_stats* st, const SlabSpec& slab)
 {
     const size_t bpp = h.getBytesPerPixel();
     const uint8_t hv = h.headerVersion;
@@ -391,6 +391,22 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
     const int T = h.Nnum;
 
     const uint16_t* d_img = (const uint16_t*)img;
+    // slab of a larger stack: its first frame may need the raw frame z0 - 1
+    const uint16_t* d_prev = nullptr;
+    if (slab.z0 > 0) {
+        if (V != 1) return 3;  // slabs are z ranges of a single (c, t) volume
+        if (video && (slab.z0 & 1)) {
+            if (!slab.prev) return 3;
+            if (dev) {
+                d_prev = (const uint16_t*)slab.prev;
+            } else {
+                if (!dev_alloc(d_prev_, d_prev_cap_, W * H * 2)) return 3;
+                if (hipMemcpyAsync(d_prev_, slab.prev, W * H * 2, hipMemcpyHostToDevice, stream_) != hipSuccess)
+                    return 3;
+                d_prev = (const uint16_t*)d_prev_;
+            }
+        }
+    }
     if (!dev && !dev_alloc(d_in_, d_in_cap_, vol * 2)) return 3;
     if (!dev_alloc(d_sym_, d_sym_cap_, (dev ? V * vol : vol) * 2)) return 3;
     if (!h_sym_ || h_sym_cap_ < total_bytes) {
@@ -431,7 +447,7 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
         }
         uint16_t* dst = (uint16_t*)d_sym_ + (dev ? v * vol : 0);
         (void)hipEventRecord(ev0_, stream_);
-        int rc = lfm_hip_predict(src, nullptr, dst, (int)W, (int)H, (int)Z, T, fam, k, video, 0, stream_);
+        int rc = lfm_hip_predict(src, d_prev, dst, (int)W, (int)H, (int)Z, T, fam, k, video, (int)slab.z0, stream_);
         (void)hipEventRecord(ev1_, stream_);
         if (rc != LFM_HIP_OK) return 3;
         if (!dev) {
@@ -461,8 +477,10 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
     return 0;
 }
 
-int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads)
+int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
+                    const SlabSpec* slab)
 {
+    static const SlabSpec whole;
     if (threads <= 0) threads = default_threads();
     auto t0 = clk::now();
     if (st) std::memset(st, 0, sizeof(*st));
@@ -477,7 +495,7 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
         return 5;
     }
     const uint8_t* sym = nullptr;
-    int rc = predictor_stage(img, dev, h, &sym, st);
+    int rc = predictor_stage(img, dev, h, &sym, st, slab ? *slab : whole);
     if (rc) return rc;
     auto tc = clk::now();
     rc = compress_blocks(sym, h, sink, threads);
@@ -503,6 +521,63 @@ Encoder& shared_encoder(std::unique_lock<std::mutex>& lock)
     dev = std::max(0, std::min(dev, 63));
     if (!enc[dev]) enc[dev].reset(new Encoder(dev));
     return *enc[dev];
+}
+
+// ------------------------------------------------------------ z-slab merge --
+int merge_slabs(const uint8_t* const* slabs, const uint64_t* lens, int n, std::vector<uint8_t>* out)
+{
+    if (n <= 0 || !slabs || !lens || !out) return 3;
+    std::vector<klb_image_header> hs(n);
+    for (int i = 0; i < n; ++i)
+        if (hs[i].parseHeader(slabs[i], lens[i])) return 3;
+    const klb_image_header& h0 = hs[0];
+    if (h0.xyzct[3] != 1 || h0.xyzct[4] != 1) return 3;
+    const uint32_t bz = h0.blockSize[2];
+    uint64_t Z = 0, nb = 0, payload = 0;
+    for (int i = 0; i < n; ++i) {
+        const klb_image_header& hi = hs[i];
+        bool same = hi.xyzct[0] == h0.xyzct[0] && hi.xyzct[1] == h0.xyzct[1] && hi.xyzct[3] == 1 &&
+                    hi.xyzct[4] == 1 && hi.dataType == h0.dataType && hi.compressionType == h0.compressionType &&
+                    hi.headerVersion == h0.headerVersion && hi.Nnum == h0.Nnum &&
+                    std::memcmp(hi.pixelSize, h0.pixelSize, sizeof(h0.pixelSize)) == 0 &&
+                    std::memcmp(hi.metadata, h0.metadata, KLB_METADATA_SIZE) == 0 &&
+                    hi.blockSize[0] == h0.blockSize[0] && hi.blockSize[1] == h0.blockSize[1];
+        if (i + 1 < n) same = same && hi.blockSize[2] == bz && hi.xyzct[2] % bz == 0;
+        else same = same && hi.blockSize[2] == std::min(bz, hi.xyzct[2]);
+        if (!same) {
+            std::printf("ERROR: slab %d does not continue slab 0 (dims, type, predictor or block depth)\n", i);
+            return 3;
+        }
+        const uint64_t hsz = hi.getSizeInBytes();
+        const uint64_t body = hi.Nb ? hi.blockOffset[hi.Nb - 1] : 0;
+        if (hsz + body > lens[i]) return 3;
+        Z += hi.xyzct[2];
+        nb += hi.Nb;
+        payload += body;
+    }
+    klb_image_header H = h0;
+    H.xyzct[2] = (uint32_t)Z;
+    H.resizeBlockOffset(H.calculateNumBlocks());
+    if (H.Nb != nb) return 3;
+    uint64_t acc = 0, b = 0;
+    for (int i = 0; i < n; ++i) {
+        uint64_t prev_end = 0;
+        for (size_t j = 0; j < hs[i].Nb; ++j) {
+            acc += hs[i].blockOffset[j] - prev_end;
+            prev_end = hs[i].blockOffset[j];
+            H.blockOffset[b++] = acc;
+        }
+    }
+    const size_t hsz = H.getSizeInBytes();
+    out->assign(hsz + payload, 0);
+    H.serialize(out->data(), hsz);
+    uint8_t* dst = out->data() + hsz;
+    for (int i = 0; i < n; ++i) {
+        const uint64_t body = hs[i].Nb ? hs[i].blockOffset[hs[i].Nb - 1] : 0;
+        std::memcpy(dst, slabs[i] + hs[i].getSizeInBytes(), body);
+        dst += body;
+    }
+    return 0;
 }
 
 // ---------------------------------------------------------------- decode --

@@ -63,6 +63,14 @@ private:
 // the clamped block size; its blockOffset table is filled.
 int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads);
 
+// z-slab [z0, z0 + xyzct[2]) of a larger stack (c = t = 1): the temporal
+// flag of frame z is video & (z0 + z), and the first frame's previous raw
+// frame is `prev` (host or device like the image) when z0 is odd.
+struct SlabSpec {
+    uint32_t z0 = 0;
+    const void* prev = nullptr;
+};
+
 // Encoder: GPU predictor stage + block compression.  One per device; keeps
 // device / pinned buffers between calls.
 class Encoder {
@@ -70,12 +78,14 @@ public:
     explicit Encoder(int device);
     ~Encoder();
     // img: host pointer (dev=false) or device pointer on this encoder's device
-    int encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads);
+    int encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
+               const SlabSpec* slab = nullptr);
     std::vector<uint8_t> mem_out;
     int device() const { return device_; }
 
 private:
-    int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, lfm_encode_stats* st);
+    int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, lfm_encode_stats* st,
+                        const SlabSpec& slab);
     int ensure_gpu();
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     int device_;
@@ -85,11 +95,19 @@ private:
     void* d_in_ = nullptr;  size_t d_in_cap_ = 0;
     void* d_sym_ = nullptr; size_t d_sym_cap_ = 0;
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
+    void* d_prev_ = nullptr; size_t d_prev_cap_ = 0;
     void* h_sym_ = nullptr; size_t h_sym_cap_ = 0;   // pinned
 };
 
 // process-wide encoder for the C ABI / klb_imageIO (serialised by its mutex)
 Encoder& shared_encoder(std::unique_lock<std::mutex>& lock);
+
+// Assemble one .lfm from the .lfm files of consecutive z-slabs of a stack
+// (each encoded with the same forced predictor, slab i starting at the sum of
+// the previous depths, depths multiples of the block depth except the last):
+// the blocks of a slab are a contiguous id range of the whole stack's blocks,
+// so the payloads concatenate and the offset table is re-accumulated.
+int merge_slabs(const uint8_t* const* slabs, const uint64_t* lens, int n, std::vector<uint8_t>* out);
 
 // Decode the payload of a .lfm (bytes after the header) into img.
 int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int threads,

@@ -34,7 +34,8 @@ EXPORTS = [
     "readKLBroiInPlace",
     # lfm_api.h
     "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
-    "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_decode_memory",
+    "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
+    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory",
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic",
@@ -92,6 +93,14 @@ def lib():
     L.lfm_encoder_encode.argtypes = [vp, vp, ctypes.c_int, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p,
                                      ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
+    L.lfm_encoder_encode_slab.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_uint32, u32p, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, u32p, ctypes.c_int, ctypes.c_char_p,
+                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
+    L.lfm_merge_slabs.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
+                                  ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_uint64)]
+    L.lfm_free.argtypes = [vp]
+    L.lfm_free.restype = None
     L.lfm_decode_memory.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_int]
     L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_predict_candidates.argtypes = [vp, vp] + [ctypes.c_int] * 4 + [vp]
@@ -228,27 +237,27 @@ class Encoder:
         except Exception:
             pass
 
-    def encode(self, img, header_version=0, nnum=13, block_size=None, compression=1, metadata=None,
-               xyzct=None, data_type=None):
-        """img: numpy array [t,c,z,y,x] (host) or a torch CUDA tensor (device, uint16 viewed as int16 ok).
-        Returns (bytes_view, stats dict)."""
-        dev = 0
+    @staticmethod
+    def _operand(img, xyzct, data_type):
+        """(pointer, is_device, xyzct, data_type, keepalive) of a numpy array or torch tensor."""
         if _HAVE_TORCH and isinstance(img, torch.Tensor):
-            if not img.is_cuda:
-                img = img.numpy()
-            else:
-                dev = 1
-                ptr = img.data_ptr()
+            if img.is_cuda:
                 shape = list(img.shape)
                 while len(shape) < 5:
                     shape = [1] + shape
                 xyzct = xyzct or [shape[4], shape[3], shape[2], shape[1], shape[0]]
-                data_type = 1 if data_type is None else data_type
-        if not dev:
-            img = np.ascontiguousarray(img)
-            ptr = img.ctypes.data
-            xyzct = xyzct or _xyzct(img)
-            data_type = DTYPES[img.dtype] if data_type is None else data_type
+                return img.data_ptr(), 1, xyzct, (1 if data_type is None else data_type), img
+            img = img.numpy()
+        img = np.ascontiguousarray(img)
+        xyzct = xyzct or _xyzct(img)
+        data_type = DTYPES[img.dtype] if data_type is None else data_type
+        return img.ctypes.data, 0, xyzct, data_type, img
+
+    def encode(self, img, header_version=0, nnum=13, block_size=None, compression=1, metadata=None,
+               xyzct=None, data_type=None):
+        """img: numpy array [t,c,z,y,x] (host) or a torch CUDA tensor (device, uint16 viewed as int16 ok).
+        Returns (bytes, stats dict)."""
+        ptr, dev, xyzct, data_type, keep = self._operand(img, xyzct, data_type)
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_uint64()
         st = EncodeStats()
@@ -256,8 +265,45 @@ class Encoder:
                                       _u32(block_size) if block_size is not None else None, compression,
                                       _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
         _check(rc, "lfm_encoder_encode")
-        buf = ctypes.string_at(out, n.value)
-        return buf, st.as_dict()
+        del keep
+        return ctypes.string_at(out, n.value), st.as_dict()
+
+    def encode_slab(self, img, z0, prev=None, header_version=8, nnum=13, block_size=None, compression=1,
+                    metadata=None, xyzct=None, data_type=None):
+        """Encode the z-slab of a larger stack that starts at global frame z0
+        (see lfm_encoder_encode_slab); prev = raw frame z0-1 (same residency
+        as img), needed when the slab starts at an odd frame of a video stack.
+        Returns (slab .lfm bytes, stats)."""
+        ptr, dev, xyzct, data_type, keep = self._operand(img, xyzct, data_type)
+        pptr = None
+        if prev is not None:
+            pptr, pdev, _, _, pkeep = self._operand(prev, [1, 1, 1, 1, 1], data_type)
+            if pdev != dev:
+                raise LfmError("prev must live where img lives (host or device)")
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_uint64()
+        st = EncodeStats()
+        rc = lib().lfm_encoder_encode_slab(self._h, ptr, dev, pptr, int(z0), _u32(xyzct), data_type,
+                                           int(header_version), int(nnum),
+                                           _u32(block_size) if block_size is not None else None, compression,
+                                           _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
+        _check(rc, "lfm_encoder_encode_slab")
+        del keep
+        return ctypes.string_at(out, n.value), st.as_dict()
+
+
+def merge_slabs(slabs):
+    """Join the .lfm bytes of consecutive z-slabs into the whole stack's .lfm."""
+    n = len(slabs)
+    arr = (ctypes.c_char_p * n)(*[bytes(b) for b in slabs])
+    lens = (ctypes.c_uint64 * n)(*[len(b) for b in slabs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    ln = ctypes.c_uint64()
+    _check(lib().lfm_merge_slabs(arr, lens, n, ctypes.byref(out), ctypes.byref(ln)), "lfm_merge_slabs")
+    try:
+        return ctypes.string_at(out, ln.value)
+    finally:
+        lib().lfm_free(out)
 
 
 def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):

@@ -160,10 +160,12 @@ def select(frame, T, family):
     return k, np.array(list(ent), dtype=np.float32)
 
 
-def predictor_stage(img, header_version, T, family):
+def predictor_stage(img, header_version, T, family, z0=0, prev=None):
     """img: (t, c, z, y, x) uint16.  Returns (symbols, header_version_out, entropies|None).
 
-    klb_imageIO.cpp:2271-2399 with the per-volume decision for c*t > 1."""
+    klb_imageIO.cpp:2271-2399 with the per-volume decision for c*t > 1.
+    z0 / prev: the stack is the z-slab starting at global frame z0 (c = t = 1)
+    and prev is raw frame z0 - 1 (multi-GPU sharding)."""
     hv = int(header_version)
     req = hv & 0x7F
     video = (hv >> 7) & 1
@@ -177,6 +179,14 @@ def predictor_stage(img, header_version, T, family):
             raise ValueError("predictor request %d is not a valid forced request" % req)
         hv_out = (hv & 0x80) | k
     sym = np.empty_like(img)
+    if z0:
+        assert img.shape[0] == 1 and img.shape[1] == 1
+        vol = img[0, 0]
+        for z in range(vol.shape[0]):
+            zf = (video & (z0 + z)) & 1
+            p = vol[z - 1] if z else prev
+            sym[0, 0, z] = predict_frame(vol[z], p if zf else None, T, family, k, zf) if k else vol[z]
+        return sym, hv_out, ent
     for t in range(img.shape[0]):
         for c in range(img.shape[1]):
             sym[t, c] = predict_volume(img[t, c], T, family, k, video)
@@ -226,8 +236,9 @@ def gather_block(arr5, coord, size):
 
 
 def encode(img, header_version=0, nnum=13, family="tiles", block_size=None, pixel_size=None,
-           metadata=None, compression=1, data_type=1):
-    """img: ndarray shaped (t, c, z, y, x) (or fewer leading dims).  Returns .lfm bytes."""
+           metadata=None, compression=1, data_type=1, z0=0, prev=None):
+    """img: ndarray shaped (t, c, z, y, x) (or fewer leading dims).  Returns .lfm bytes.
+    z0 / prev: encode the z-slab starting at global frame z0 (see predictor_stage)."""
     img = np.asarray(img)
     while img.ndim < 5:
         img = img[None]
@@ -237,7 +248,7 @@ def encode(img, header_version=0, nnum=13, family="tiles", block_size=None, pixe
     bs = [min(b, x) for b, x in zip(bs, xyzct)]                       # :2402-2404
     ps = list(pixel_size) if pixel_size is not None else [1.0] * 5
     if bpp == 2 and compression in (0, 1, 2):
-        sym, hv, _ = predictor_stage(img.view(np.uint16), header_version, nnum, family)
+        sym, hv, _ = predictor_stage(img.view(np.uint16), header_version, nnum, family, z0, prev)
     else:
         sym, hv = img, header_version & 0x80
     block_bytes = bpp * int(np.prod(bs))

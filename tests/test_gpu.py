@@ -215,3 +215,34 @@ def test_synth_generator_matches_numpy(lfmlib, oracle, gpu):
         lfmlib.synth_device(d, X, Y, Z, T, seed=0x4C464D03)
         torch.cuda.synchronize()
         assert np.array_equal(host16(d), oracle.synthetic_lf(X, Y, Z=Z, T=T, seed=0x4C464D03)[0, 0])
+
+
+@pytest.mark.parametrize("fam,video,on_device", [("tiles", True, True), ("tiles", True, False),
+                                                 ("angle", False, True)])
+def test_slab_encode_and_merge(lfmlib, oracle, gpu, fam, video, on_device):
+    """Multi-GPU sharding on one GPU: z-slabs (odd starts with the previous
+    raw frame) encoded with the forced predictor, then joined: identical to
+    the oracle's one-piece auto-selected encode."""
+    from lfm.shard import forced_request, plan_slabs
+    torch = gpu
+    Z, bs = 20, [64, 32, 3, 1, 1]  # slabs (0, 9), (9, 9), (18, 2): an odd start
+    img = oracle.synthetic_lf(200, 96, Z=Z, T=13, seed=0x4C464D08)
+    full = oracle.encode(img, header_version=(0x80 if video else 0), nnum=13, family=fam, block_size=bs)
+    lfmlib.set_family(fam)
+    try:
+        enc = lfmlib.Encoder(device=0)
+        k, _ = lfmlib.select_device(dev16(torch, img[0, 0, 0]), 200, 96, 13, fam)
+        slabs = []
+        for z0, d in plan_slabs(Z, 3, 3):
+            slab = img[0, 0, z0:z0 + d]
+            prev = img[0, 0, z0 - 1] if z0 else None
+            if on_device:
+                slab = dev16(torch, slab)
+                prev = dev16(torch, prev) if prev is not None else None
+            b, st = enc.encode_slab(slab, z0, prev=prev, header_version=forced_request(k, video), nnum=13,
+                                    block_size=bs)
+            slabs.append(b)
+        enc.close()
+    finally:
+        lfmlib.set_family("tiles")
+    assert lfmlib.merge_slabs(slabs) == full
