@@ -62,6 +62,18 @@ size_t lfm_hip_select_workspace_bytes(int W, int H);
 int lfm_hip_select(const uint16_t* d_frame, int W, int H, int T, int family, float entropy[8], int* chosen,
                    void* d_workspace, void* stream);
 
+/* bzip2 (libbzip2 1.0.6 byte-exact) of the blocks [first, first + count) of
+ * the x-fastest block grid of a device image (dims / bs as in the .lfm
+ * header, bpp bytes per sample) at `level`: the compressed streams land
+ * back to back in d_payload (block order); h_sizes[i] / h_flags[i] per
+ * stream (flag != 0: the stream is NOT in the payload and must be produced by
+ * the host library -- RLE1 block reaching nblockMAX, or a periodic block).
+ * d_ws: lfm_hip_bzip2_workspace_bytes(count, blockBytes).  Synchronous. */
+size_t lfm_hip_bzip2_workspace_bytes(uint32_t count, uint32_t block_bytes);
+int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], const uint32_t bs[5], uint32_t bpp,
+                         uint32_t first, uint32_t count, uint32_t level, void* d_ws, size_t ws_bytes,
+                         void* d_payload, uint64_t* h_sizes, uint32_t* h_flags, void* stream);
+
 /* Synthetic light-field stack of SURVEY.md 8(d) (integer generator) written
  * straight into device memory: X*Y*Z pixels of volume (c, t) = (0, t_index),
  * global pixel index offset idx0 (for z-slabs of a larger stack). */

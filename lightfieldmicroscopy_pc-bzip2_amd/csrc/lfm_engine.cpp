@@ -291,6 +291,17 @@ int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int thr
 }
 
 // --------------------------------------------------------------- encoder --
+// GPU bzip2 (default when a GPU is usable); env LFM_GPU_BZIP2=0 selects the
+// host library for every block (the same bytes, for comparison).
+bool gpu_bzip2_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("LFM_GPU_BZIP2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 Encoder::Encoder(int device) : device_(device) {}
 
 Encoder::~Encoder()
@@ -300,6 +311,10 @@ Encoder::~Encoder()
         if (d_in_) (void)hipFree(d_in_);
         if (d_sym_) (void)hipFree(d_sym_);
         if (d_ws_) (void)hipFree(d_ws_);
+        if (d_prev_) (void)hipFree(d_prev_);
+        if (d_bz_ws_) (void)hipFree(d_bz_ws_);
+        if (d_bz_out_) (void)hipFree(d_bz_out_);
+        if (h_bz_out_) (void)hipHostFree(h_bz_out_);
         if (h_sym_) (void)hipHostFree(h_sym_);
         if (ev0_) (void)hipEventDestroy(ev0_);
         if (ev1_) (void)hipEventDestroy(ev1_);
@@ -338,8 +353,11 @@ void* Encoder::dev_alloc(void*& p, size_t& cap, size_t need)
 }
 
 int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym,
-                             lfm_encode_stats* st, const SlabSpec& slab)
+                             const uint8_t** dsym, lfm_encode_stats* st, const SlabSpec& slab)
 {
+    // dsym != nullptr: the caller compresses on the GPU -- leave the symbols
+    // of every volume in device memory (*dsym) and skip the host copy.
+    const bool keep = dsym != nullptr;
     const size_t bpp = h.getBytesPerPixel();
     const uint8_t hv = h.headerVersion;
     const int req = hv & 0x7F;
@@ -351,6 +369,8 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
     const bool autosel = req < NUM_PREDICTORS;
     int k = autosel ? 0 : (hv & 0x77);  // `headerVersion & 0x7F - 8` parses as & 0x77 (klb_imageIO.cpp:2380)
     if (st) st->chosen = 0;
+    if (sym) *sym = nullptr;
+    if (dsym) *dsym = nullptr;
 
     auto host_symbols_from_device = [&](const void* d, size_t bytes) -> int {
         if (!h_sym_ || h_sym_cap_ < bytes) {
@@ -374,11 +394,23 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
     if (!predictable || (!autosel && k == 0)) {
         if (!autosel && k > 7) return kErrBadPredictor;
         h.headerVersion = (uint8_t)(hv & 0x80);
+        if (keep) {  // the raw image is the symbol stream
+            if (dev) {
+                *dsym = (const uint8_t*)img;
+                return 0;
+            }
+            if (!dev_alloc(d_sym_, d_sym_cap_, total_bytes)) return 3;
+            auto t0 = clk::now();
+            if (hipMemcpyAsync(d_sym_, img, total_bytes, hipMemcpyHostToDevice, stream_) != hipSuccess) return 3;
+            if (hipStreamSynchronize(stream_) != hipSuccess) return 3;
+            if (st) st->h2d_ms += ms_since(t0);
+            *dsym = (const uint8_t*)d_sym_;
+            return 0;
+        }
         if (!dev) {
             *sym = (const uint8_t*)img;
             return 0;
         }
-        if (int rc = ensure_gpu()) return rc;
         return host_symbols_from_device(img, total_bytes);
     }
     if (!autosel && k > 7) {
@@ -407,9 +439,12 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
             }
         }
     }
+    // every volume's symbols stay on the device when they are needed there
+    // (device input, or GPU compression); otherwise one volume at a time
+    const bool all_on_device = dev || keep;
     if (!dev && !dev_alloc(d_in_, d_in_cap_, vol * 2)) return 3;
-    if (!dev_alloc(d_sym_, d_sym_cap_, (dev ? V * vol : vol) * 2)) return 3;
-    if (!h_sym_ || h_sym_cap_ < total_bytes) {
+    if (!dev_alloc(d_sym_, d_sym_cap_, (all_on_device ? V * vol : vol) * 2)) return 3;
+    if (!keep && (!h_sym_ || h_sym_cap_ < total_bytes)) {
         if (h_sym_) (void)hipHostFree(h_sym_);
         h_sym_ = nullptr;
         h_sym_cap_ = 0;
@@ -445,12 +480,12 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
                 std::memcpy(st->entropy, ent, sizeof(ent));
             }
         }
-        uint16_t* dst = (uint16_t*)d_sym_ + (dev ? v * vol : 0);
+        uint16_t* dst = (uint16_t*)d_sym_ + (all_on_device ? v * vol : 0);
         (void)hipEventRecord(ev0_, stream_);
         int rc = lfm_hip_predict(src, d_prev, dst, (int)W, (int)H, (int)Z, T, fam, k, video, (int)slab.z0, stream_);
         (void)hipEventRecord(ev1_, stream_);
         if (rc != LFM_HIP_OK) return 3;
-        if (!dev) {
+        if (!all_on_device) {
             auto t0 = clk::now();
             if (hipMemcpyAsync((uint8_t*)h_sym_ + v * vol * 2, dst, vol * 2, hipMemcpyDeviceToHost, stream_) !=
                 hipSuccess)
@@ -464,17 +499,111 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
         (void)hipEventElapsedTime(&ms, ev0_, ev1_);
         pred_ms_total += ms;
     }
+    if (st) st->predict_ms += pred_ms_total;
+    h.headerVersion = (uint8_t)((hv & 0x80) | k);
+    if (st) st->chosen = k;
+    if (keep) {
+        *dsym = (const uint8_t*)d_sym_;
+        return 0;
+    }
     if (dev) {
         auto t0 = clk::now();
         if (hipMemcpyAsync(h_sym_, d_sym_, total_bytes, hipMemcpyDeviceToHost, stream_) != hipSuccess) return 3;
         if (hipStreamSynchronize(stream_) != hipSuccess) return 3;
         if (st) st->d2h_ms += ms_since(t0);
     }
-    if (st) st->predict_ms += pred_ms_total;
-    h.headerVersion = (uint8_t)((hv & 0x80) | k);
-    if (st) st->chosen = k;
     *sym = (const uint8_t*)h_sym_;
     return 0;
+}
+
+// GPU bzip2 of every block (lfm_bzip2.hip), streams batched to bound the
+// workspace; streams the device hands back (RLE1 block reaching nblockMAX,
+// periodic blocks) are compressed by libbz2 here.  Same bytes either way.
+int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st)
+{
+    const BlockGrid g(h);
+    const uint64_t nblocks = g.nblocks;
+    h.resizeBlockOffset(nblocks);
+    const size_t bpp = h.getBytesPerPixel();
+    const uint32_t block_bytes = h.getBlockSizeBytes();
+    const int level = std::min(9, (int)((block_bytes + 99999) / 100000));  // klb_imageIO.cpp:108
+    const size_t out_cap = ((size_t)block_bytes + block_bytes / 50 + 4096 + 255) / 256 * 256;
+    // batch: bounded by a workspace budget (env LFM_BZ2_GPU_BUDGET_MB, default 24 GiB)
+    static const size_t budget = [] {
+        const char* e = std::getenv("LFM_BZ2_GPU_BUDGET_MB");
+        const long v = e ? std::atol(e) : 0;
+        return (size_t)(v > 0 ? v : 24 * 1024) << 20;
+    }();
+    const size_t per_stream = lfm_hip_bzip2_workspace_bytes(1, block_bytes) + out_cap;
+    uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, budget / per_stream));
+    if (batch * ((block_bytes + block_bytes / 4 + 64 + 255) / 256 * 256) >= (1ull << 32))
+        batch = ((1ull << 32) - 1) / ((block_bytes + block_bytes / 4 + 64 + 255) / 256 * 256);
+    const size_t ws = lfm_hip_bzip2_workspace_bytes((uint32_t)batch, block_bytes);
+    if (!dev_alloc(d_bz_ws_, d_bz_ws_cap_, ws)) return 3;
+    if (!dev_alloc(d_bz_out_, d_bz_out_cap_, batch * out_cap)) return 3;
+    if (!h_bz_out_ || h_bz_out_cap_ < batch * out_cap) {
+        if (h_bz_out_) (void)hipHostFree(h_bz_out_);
+        h_bz_out_ = nullptr;
+        h_bz_out_cap_ = 0;
+        if (hipHostMalloc(&h_bz_out_, batch * out_cap, hipHostMallocDefault) != hipSuccess) return 3;
+        h_bz_out_cap_ = batch * out_cap;
+    }
+    uint32_t dims[5], bs[5];
+    for (int d = 0; d < 5; ++d) {
+        dims[d] = h.xyzct[d];
+        bs[d] = h.blockSize[d];
+    }
+    std::vector<uint64_t> sizes(batch);
+    std::vector<uint32_t> flags(batch);
+    const uint8_t* h_all = nullptr;  // host copy of the symbols, only if a stream needs the host library
+    std::vector<uint8_t> in(block_bytes), out((size_t)std::ceil((float)block_bytes * 2.0f + 50.0f));
+    int rc = sink.begin(h);
+    uint64_t offset = 0;
+    for (uint64_t b0 = 0; b0 < nblocks && !rc; b0 += batch) {
+        const uint32_t cnt = (uint32_t)std::min<uint64_t>(batch, nblocks - b0);
+        if (lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, d_bz_ws_, ws,
+                                 d_bz_out_, sizes.data(), flags.data(), stream_) != LFM_HIP_OK)
+            return 3;
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < cnt; ++i) tot += sizes[i];
+        auto t0 = clk::now();
+        if (hipMemcpyAsync(h_bz_out_, d_bz_out_, tot, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
+            hipStreamSynchronize(stream_) != hipSuccess)
+            return 3;
+        if (st) st->d2h_ms += ms_since(t0);
+        const uint8_t* p = (const uint8_t*)h_bz_out_;
+        for (uint32_t i = 0; i < cnt && !rc; ++i) {
+            if (flags[i]) {
+                if (!h_all) {
+                    const size_t bytes = h.getImageSizeBytes();
+                    if (!h_sym_ || h_sym_cap_ < bytes) {
+                        if (h_sym_) (void)hipHostFree(h_sym_);
+                        h_sym_ = nullptr;
+                        h_sym_cap_ = 0;
+                        if (hipHostMalloc(&h_sym_, bytes, hipHostMallocDefault) != hipSuccess) return 3;
+                        h_sym_cap_ = bytes;
+                    }
+                    if (hipMemcpyAsync(h_sym_, d_sym, bytes, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
+                        hipStreamSynchronize(stream_) != hipSuccess)
+                        return 3;
+                    h_all = (const uint8_t*)h_sym_;
+                }
+                size_t n = 0;
+                gather_block(h_all, g, b0 + i, bpp, in.data(), &n);
+                uint32_t len = 0;
+                rc = compress_one(BZIP2, in.data(), (uint32_t)n, out.data(), (uint32_t)out.size(), &len, level);
+                if (!rc) rc = sink.append(out.data(), len);
+                offset += len;
+            } else {
+                rc = sink.append(p, sizes[i]);
+                p += sizes[i];
+                offset += sizes[i];
+            }
+            h.blockOffset[b0 + i] = offset;
+        }
+    }
+    if (rc) return rc;
+    return sink.finish(h);
 }
 
 int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
@@ -495,10 +624,17 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
         return 5;
     }
     const uint8_t* sym = nullptr;
-    int rc = predictor_stage(img, dev, h, &sym, st, slab ? *slab : whole);
+    const uint8_t* dsym = nullptr;
+    const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
+    int rc = predictor_stage(img, dev, h, &sym, gpu_bz ? &dsym : nullptr, st, slab ? *slab : whole);
     if (rc) return rc;
     auto tc = clk::now();
-    rc = compress_blocks(sym, h, sink, threads);
+    if (gpu_bz) {
+        if ((rc = ensure_gpu())) return rc;
+        rc = gpu_compress(dsym, h, sink, st);
+    } else {
+        rc = compress_blocks(sym, h, sink, threads);
+    }
     if (st) {
         st->compress_ms = ms_since(tc);
         st->total_ms = ms_since(t0);

@@ -16,6 +16,7 @@ namespace lfm {
 constexpr int kErrBadPredictor = 6;
 constexpr int kErrNoGpu = 7;
 
+bool gpu_bzip2_enabled();   // env LFM_GPU_BZIP2 (default on)
 int default_threads();      // env LFM_NUM_THREADS, else OMP_NUM_THREADS, else hardware_concurrency
 int current_family();       // lfm_set_family / env LFM_PREDICTOR_WAY / LFM_PREDICTOR_WAY
 void set_family(int fam);
@@ -84,8 +85,9 @@ public:
     int device() const { return device_; }
 
 private:
-    int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, lfm_encode_stats* st,
-                        const SlabSpec& slab);
+    int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, const uint8_t** dsym,
+                        lfm_encode_stats* st, const SlabSpec& slab);
+    int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st);
     int ensure_gpu();
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     int device_;
@@ -96,6 +98,9 @@ private:
     void* d_sym_ = nullptr; size_t d_sym_cap_ = 0;
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
     void* d_prev_ = nullptr; size_t d_prev_cap_ = 0;
+    void* d_bz_ws_ = nullptr; size_t d_bz_ws_cap_ = 0;
+    void* d_bz_out_ = nullptr; size_t d_bz_out_cap_ = 0;
+    void* h_bz_out_ = nullptr; size_t h_bz_out_cap_ = 0;  // pinned
     void* h_sym_ = nullptr; size_t h_sym_cap_ = 0;   // pinned
 };
 

@@ -38,7 +38,8 @@ EXPORTS = [
     "lfm_merge_slabs", "lfm_free", "lfm_decode_memory",
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
-    "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic",
+    "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
+    "lfm_hip_bzip2_blocks",
 ]
 
 
@@ -105,6 +106,11 @@ def lib():
     L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_predict_candidates.argtypes = [vp, vp] + [ctypes.c_int] * 4 + [vp]
     L.lfm_hip_entropy2d.argtypes = [vp, ctypes.c_uint64, f32p, vp]
+    L.lfm_hip_bzip2_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.lfm_hip_bzip2_workspace_bytes.restype = ctypes.c_size_t
+    L.lfm_hip_bzip2_blocks.argtypes = [vp, u32p, u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.c_uint32, vp, ctypes.c_size_t, vp,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), vp]
     L.lfm_hip_select_workspace_bytes.restype = ctypes.c_size_t
     L.lfm_hip_select_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     L.lfm_hip_select.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p,
@@ -353,6 +359,35 @@ def entropy_device(d_cand, npix=None, stream=None):
     n = d_cand.numel() if npix is None else npix
     _check(lib().lfm_hip_entropy2d(d_cand.data_ptr(), n, ctypes.byref(e), _stream(stream)), "lfm_hip_entropy2d")
     return e.value
+
+
+def bzip2_device(d_img, dims, block, bpp, level=None, first=0, count=None, stream=None):
+    """GPU bzip2 of the x-fastest block grid of a device image (torch tensor
+    holding dims[4]*...*dims[0]*bpp bytes).  Returns ([bytes or None per
+    stream], flags): None where the stream was handed to the host library."""
+    nb = [-(-d // b) for d, b in zip(dims, block)]
+    total = int(np.prod(nb))
+    count = total - first if count is None else count
+    block_bytes = int(np.prod(block)) * bpp
+    level = min(9, -(-block_bytes // 100000)) if level is None else level
+    ws_bytes = lib().lfm_hip_bzip2_workspace_bytes(count, block_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=d_img.device)
+    out_cap = ((block_bytes + block_bytes // 50 + 4096 + 255) // 256) * 256
+    pay = torch.empty(count * out_cap, dtype=torch.uint8, device=d_img.device)
+    sizes = (ctypes.c_uint64 * count)()
+    flags = (ctypes.c_uint32 * count)()
+    _check(lib().lfm_hip_bzip2_blocks(d_img.data_ptr(), _u32(dims), _u32(block), bpp, first, count, level,
+                                      ws.data_ptr(), ws_bytes, pay.data_ptr(), sizes, flags, _stream(stream)),
+           "lfm_hip_bzip2_blocks")
+    host = pay[:int(sum(sizes))].cpu().numpy().tobytes()
+    out, o = [], 0
+    for i in range(count):
+        if flags[i]:
+            out.append(None)
+        else:
+            out.append(host[o:o + sizes[i]])
+            o += sizes[i]
+    return out, list(flags)
 
 
 def synth_device(d_out, X, Y, Z, T, t_index=0, idx0=0, seed=0x4C464D00, stream=None):

@@ -246,3 +246,62 @@ def test_slab_encode_and_merge(lfmlib, oracle, gpu, fam, video, on_device):
     finally:
         lfmlib.set_family("tiles")
     assert lfmlib.merge_slabs(slabs) == full
+
+
+def _bz2_cases():
+    rng = np.random.default_rng(7)
+    cases = {
+        "random": rng.integers(0, 256, 40000, dtype=np.uint8),
+        "zeros": np.zeros(30000, np.uint8),
+        "one_byte": np.array([65], np.uint8),
+        "two_bytes": np.array([1, 2], np.uint8),
+        "seven": np.array([3, 3, 3, 3, 3, 3, 9], np.uint8),
+        "small_alpha": rng.integers(0, 3, 20000, dtype=np.uint8),
+        "few_syms": np.repeat(rng.integers(0, 5, 300, dtype=np.uint8), 7),
+        "periodic": np.tile(np.array([7, 9], np.uint8), 5000),
+        "periodic_runs": np.tile(np.array([1, 1, 1, 1, 1, 2], np.uint8), 3000),
+    }
+    runs = []
+    for L in (1, 2, 3, 4, 5, 254, 255, 256, 259, 510, 511, 1000):
+        runs.append(np.full(L, L % 251, np.uint8))
+        runs.append(np.array([200], np.uint8))
+    cases["run_lengths"] = np.concatenate(runs)
+    allb = np.concatenate([np.full(1 + (i % 7), i, np.uint8) for i in range(256)] * 20 + [np.array([5], np.uint8)])
+    cases["all_bytes"] = allb  # every byte value in use (not periodic: one extra byte)
+    return cases
+
+
+def test_gpu_bzip2_matches_libbz2_edge_cases(lfmlib, gpu):
+    """Every GPU stream equals libbzip2 at the same level (python's bz2 is the
+    system libbz2 1.0.8, byte-identical to the reference's 1.0.6 on the KATs);
+    periodic blocks come back flagged for the host library."""
+    import bz2
+    torch = gpu
+    for name, data in _bz2_cases().items():
+        n = len(data)
+        d = torch.from_numpy(data.copy()).cuda()
+        for level in (1, 2, 9):
+            got, flags = lfmlib.bzip2_device(d, [n, 1, 1, 1, 1], [n, 1, 1, 1, 1], 1, level=level)
+            exp = bz2.compress(data.tobytes(), level)
+            if flags[0]:
+                assert name.startswith("periodic"), (name, level)
+                continue
+            assert not name.startswith("periodic"), name
+            assert got[0] == exp, (name, level, len(got[0]), len(exp))
+
+
+def test_gpu_bzip2_block_grid_and_symbols(lfmlib, oracle, gpu):
+    """Many streams from a 2-D block grid of predicted light-field symbols
+    (border blocks, uint16 samples) against libbzip2 per block."""
+    import bz2
+    torch = gpu
+    img = oracle.synthetic_lf(200, 150, Z=5, T=13, seed=21)[0, 0]
+    sym = oracle.predict_volume(img, 13, "tiles", 4, 0)
+    d = torch.from_numpy(sym.view(np.int16).copy()).cuda()
+    dims, bs = [200, 150, 5, 1, 1], [64, 48, 2, 1, 1]
+    got, flags = lfmlib.bzip2_device(d, dims, bs, 2)
+    blocks = list(oracle.iter_blocks(dims, bs))
+    assert len(got) == len(blocks)
+    for (i, coord, size), g in zip(blocks, got):
+        raw = oracle.gather_block(sym[None, None], coord, size)
+        assert g == bz2.compress(raw, 1), i
