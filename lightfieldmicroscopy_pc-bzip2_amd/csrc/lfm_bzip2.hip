@@ -37,7 +37,13 @@
 // block) or that are periodic are flagged for the host library: the output
 // stays byte-identical in every case.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -91,6 +97,10 @@ struct Batch {
     uint32_t* vals_a;        // rotation start indices (input of a sort)
     uint32_t* sa;            // sorted rotation starts (output of a sort)
     uint32_t* rank;
+    uint32_t* vals_b;        // sorted values of the compacted rounds
+    uint32_t* cl0;           // slots of unresolved rotations (compacted)
+    uint32_t* cl1;
+    uint8_t* uflag;          // per slot / per compacted entry: still tied
     uint32_t* seg_begin;
     uint32_t* seg_end;
     uint16_t* mtfv;          // cap + 1 per stream
@@ -170,6 +180,20 @@ __device__ __forceinline__ RunSum run_combine(const RunSum& a, const RunSum& b)
     return r;
 }
 
+// Visit the bytes p[0 .. len) in order with 16-byte loads (p 16-byte aligned;
+// the load may read up to 15 bytes past len, inside the stream's buffer).
+template <typename F>
+__device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f)
+{
+    for (uint32_t k = 0; k < len; k += 16) {
+        const uint4 v = *(const uint4*)(p + k);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t b = 0; b < 16; ++b)
+            if (k + b < len) f((w[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+    }
+}
+
 // bzip2's run state machine over one chunk, started from the carried state.
 // Emission happens when a run ends (a different byte, or the 255 cap).
 template <bool WRITE>
@@ -194,8 +218,7 @@ __device__ __forceinline__ uint32_t rle_chunk(const uint8_t* p, uint32_t len, ui
             w += 5;
         }
     };
-    for (uint32_t i = 0; i < len; ++i) {
-        const uint32_t c = p[i];
+    for_bytes(p, len, [&](uint32_t c) {
         if (c != ch || rl == 255) {
             if (ch < 256) emit(ch, rl);
             ch = c;
@@ -203,7 +226,7 @@ __device__ __forceinline__ uint32_t rle_chunk(const uint8_t* p, uint32_t len, ui
         } else {
             ++rl;
         }
-    }
+    });
     return w;
 }
 
@@ -226,23 +249,30 @@ __global__ __launch_bounds__(kRleThreads) void rle1_crc(Batch B)
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     const uint32_t L = B.raw_len[s];
     const uint8_t* raw = B.raw + (size_t)s * B.raw_cap;
-    const uint32_t per = (L + kRleThreads - 1) / kRleThreads;
+    const uint32_t per = ((L + kRleThreads - 1) / kRleThreads + 15) & ~15u;  // 16-byte aligned chunks
     const uint32_t c0 = min(L, t * per), c1 = min(L, c0 + per);
     const uint32_t clen = c1 - c0;
     if (t < 8) inuse[t] = 0;
-    // chunk run summary + chunk CRC (from a zero register)
+    // chunk run summary + chunk CRC (from a zero register), one pass
     RunSum rs{clen, 0, 0, 0, 0};
     uint32_t cc = 0;
     if (clen) {
-        rs.first = raw[c0];
-        rs.last = raw[c1 - 1];
-        uint32_t i = 0;
-        while (i < clen && raw[c0 + i] == rs.first) ++i;
-        rs.lead = i;
-        i = 0;
-        while (i < clen && raw[c1 - 1 - i] == rs.last) ++i;
-        rs.trail = i;
-        for (uint32_t k = c0; k < c1; ++k) cc = crc_feed(cc, raw[k]);
+        bool lead_open = true;
+        uint32_t first = 256, prev = 256, lead = 0, trail = 0;
+        for_bytes(raw + c0, clen, [&](uint32_t b) {
+            if (first == 256) first = b;
+            if (lead_open) {
+                if (b == first) ++lead;
+                else lead_open = false;
+            }
+            trail = (b == prev) ? trail + 1 : 1;
+            prev = b;
+            cc = crc_feed(cc, b);
+        });
+        rs.first = first;
+        rs.last = prev;
+        rs.lead = lead;
+        rs.trail = trail;
     }
     sums[t] = rs;
     crcs[t] = cc;
@@ -338,7 +368,13 @@ __global__ __launch_bounds__(kRleThreads) void rle1_crc(Batch B)
 }
 
 // ------------------------------------------------------------------ BWT --
-// keys: the first 8 bytes of rotation i (big endian), value i
+// Sort values carry the rotation start i (bits 0-23, n < 2^20) and the byte
+// preceding it (bits 24-31): after sorting, that byte IS the BWT output
+// column, so the MTF stage reads it in sorted order without a gather.
+constexpr uint32_t kIdxMask = 0x00FFFFFFu;
+constexpr uint32_t kKeyBytes = 6;  // first-round key: 6 bytes (2.4 % of rotations tie; 8 bytes: 6 more passes for 0.01 %)
+
+// keys: the first kKeyBytes bytes of rotation i (big endian)
 __global__ __launch_bounds__(256) void bwt_init_keys(Batch B)
 {
     const uint32_t s = blockIdx.y;
@@ -349,98 +385,138 @@ __global__ __launch_bounds__(256) void bwt_init_keys(Batch B)
         uint64_t k = 0;
         uint32_t j = i;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (uint32_t q = 0; q < kKeyBytes; ++q) {
             k = (k << 8) | T[j];
             j = j + 1 == n ? 0 : j + 1;
         }
         B.keys_a[(size_t)s * B.cap + i] = k;
-        B.vals_a[(size_t)s * B.cap + i] = i;
+        B.vals_a[(size_t)s * B.cap + i] = i | ((uint32_t)T[i ? i - 1 : n - 1] << 24);
     }
 }
 
-// After a sort (keys_b, sa): rank[sa[j]] = first sorted position of j's
-// group.  Marks the stream done when every group is a singleton; flags a
-// periodic block when h already covers the whole rotation.
-__global__ __launch_bounds__(1024) void bwt_rank(Batch B, uint32_t covered)
+// After the first sort (keys_b = 6-byte prefixes, sa): rank[sa[j]] = first
+// sorted position of j's group, uflag[slot] = 1 where j's group has more than
+// one rotation.  Tiles of 1024 consecutive positions keep every load
+// coalesced; the group start is a running max carried across tiles.
+__global__ __launch_bounds__(1024) void bwt_rank0(Batch B)
 {
-    __shared__ uint32_t part[1024];
-    __shared__ uint32_t heads_total;
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
-    if (B.done[s]) return;
+    __shared__ uint32_t wmax[16];
+    __shared__ uint32_t carry;
+    const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
     const size_t o = (size_t)s * B.cap;
     const uint64_t* K = B.keys_b + o;
     const uint32_t* SA = B.sa + o;
-    uint32_t* R = B.rank + o;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t j0 = min(n, t * per), j1 = min(n, j0 + per);
-    uint32_t mx = 0, heads = 0;
-    for (uint32_t j = j0; j < j1; ++j)
-        if (j == 0 || K[j] != K[j - 1]) { mx = j; ++heads; }
-    if (t == 0) heads_total = 0;
-    part[t] = (j1 > j0 && (heads || t == 0)) ? mx : 0u;
+    if (t == 0) carry = 0;
     __syncthreads();
-    atomicAdd(&heads_total, heads);
-    // inclusive max-scan of group starts over threads
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] = max(part[t], v);
-        __syncthreads();
-    }
-    uint32_t g = t ? part[t - 1] : 0u;
-    for (uint32_t j = j0; j < j1; ++j) {
-        if (j == 0 || K[j] != K[j - 1]) g = j;
-        R[SA[j]] = g;
-    }
-    __syncthreads();
-    if (t == 0) {
-        if (heads_total == n) {
-            B.done[s] = 1;
-            B.seg_end[s] = B.seg_begin[s];
-        } else if (covered >= n) {  // equal rotations: periodic block
-            B.done[s] = 1;
-            B.flags[s] |= kFlagHost;
-            B.seg_end[s] = B.seg_begin[s];
+    for (uint32_t j0 = 0; j0 < n; j0 += 1024) {
+        const uint32_t j = j0 + t;
+        bool head = false, next_head = true;
+        if (j < n) {
+            const uint64_t k = K[j];
+            head = j == 0 || k != K[j - 1];
+            next_head = j + 1 >= n || K[j + 1] != k;
         }
+        uint32_t v = head ? j : 0u;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t u = __shfl_up(v, off);
+            if ((int)lane >= off) v = max(v, u);
+        }
+        if (lane == 63) wmax[wave] = v;
+        __syncthreads();
+        uint32_t pre = carry;
+        for (uint32_t w = 0; w < wave; ++w) pre = max(pre, wmax[w]);
+        const uint32_t g = max(pre, v);
+        if (j < n) {
+            B.rank[o + (SA[j] & kIdxMask)] = g;
+            B.uflag[o + j] = (head && next_head) ? 0 : 1;
+        }
+        __syncthreads();
+        if (t == 1023) carry = g;
+        __syncthreads();
     }
 }
 
-// keys for the next doubling round: (rank[i], rank[i + h]) in 20-bit fields
-__global__ __launch_bounds__(256) void bwt_double_keys(Batch B, uint32_t h)
+// keys of a compacted doubling round: (stream slot of the group start,
+// rank[i + h]) -- groups never mix, and inside a group the order is by the
+// rank of the rotation h further on
+__global__ __launch_bounds__(256) void bwt_comp_keys(Batch B, const uint32_t* __restrict__ cl,
+                                                     const uint32_t* __restrict__ cnt_p, uint32_t h)
 {
-    const uint32_t s = blockIdx.y;
-    if (B.done[s]) return;
-    const uint32_t n = B.n[s];
-    const size_t o = (size_t)s * B.cap;
-    const uint32_t hh = h % n;
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const uint32_t i = B.sa[o + j];
-        uint32_t i2 = i + hh;
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        const uint32_t slot = cl[c];
+        const uint32_t s = slot / B.cap;
+        const size_t o = (size_t)s * B.cap;
+        const uint32_t n = B.n[s];
+        const uint32_t v = B.sa[slot];
+        const uint32_t i = v & kIdxMask;
+        uint32_t i2 = i + (h % n);
         if (i2 >= n) i2 -= n;
-        B.keys_a[o + j] = ((uint64_t)B.rank[o + i] << 20) | B.rank[o + i2];
-        B.vals_a[o + j] = i;
+        B.keys_a[c] = ((uint64_t)(o + B.rank[o + i]) << 20) | B.rank[o + i2];
+        B.vals_a[c] = v;
     }
+}
+
+// write the refined order back into sa and mark the new group heads
+__global__ __launch_bounds__(256) void bwt_comp_heads(Batch B, const uint32_t* __restrict__ cl,
+                                                      const uint32_t* __restrict__ cnt_p, uint32_t* __restrict__ hv)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        B.sa[cl[c]] = B.vals_b[c];
+        const bool head = c == 0 || B.keys_b[c] != B.keys_b[c - 1];
+        hv[c] = head ? cl[c] : 0u;
+    }
+}
+
+// new ranks (slot of the new group head) and the still-tied flags
+__global__ __launch_bounds__(256) void bwt_comp_rank(Batch B, const uint32_t* __restrict__ cnt_p,
+                                                     const uint32_t* __restrict__ hvs)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        const uint32_t head_slot = hvs[c];
+        const uint32_t s = head_slot / B.cap;
+        const size_t o = (size_t)s * B.cap;
+        B.rank[o + (B.vals_b[c] & kIdxMask)] = (uint32_t)(head_slot - o);
+        const bool head = c == 0 || B.keys_b[c] != B.keys_b[c - 1];
+        const bool next_head = c + 1 >= cnt || B.keys_b[c + 1] != B.keys_b[c];
+        B.uflag[c] = (head && next_head) ? 0 : 1;
+    }
+}
+
+// rotations still tied after h covers the whole block: equal rotations of a
+// periodic block -> the host library produces that stream
+__global__ __launch_bounds__(256) void bwt_flag_periodic(Batch B, const uint32_t* __restrict__ cl,
+                                                         const uint32_t* __restrict__ cnt_p)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x)
+        atomicOr(&B.flags[cl[c] / B.cap], kFlagHost);
 }
 
 // ------------------------------------------------------------------ MTF --
-// One wave per stream.  yy[4l .. 4l+3] live in lane l's word (byte k = entry
-// 4l+k); lookups by the zero-byte trick and a ballot.
-__global__ __launch_bounds__(256) void mtf_rle2(Batch B)
+// compress.c generateMTFValues in three parallel steps.  The move-to-front
+// list in front of position j is a function of the last occurrences before
+// j: symbols ordered by their last occurrence (most recent first), then the
+// never-seen symbols in their initial order.  So every 4096-symbol segment of
+// a stream can run its own MTF once those last occurrences are known:
+//   mtf_last    per segment: the sorted symbols ll[j] (inUse-mapped bytes
+//               before each sorted rotation) and each symbol's last position
+//   mtf_prefix  per stream: exclusive running max over the segments
+//   mtf_seg     per segment, one wave: initial list from the ranks of those
+//               positions, then the sequential MTF (list packed 4 entries per
+//               lane; lookups by ballot, shifts by a one-lane wave rotate)
+//   rle2        per stream: zero runs -> RUNA/RUNB digits, v -> v + 1, EOB,
+//               symbol frequencies (the run state is carried across thread
+//               chunks by a scan, as in rle1_crc)
+constexpr uint32_t kSeg = 4096;
+
+__device__ __forceinline__ void make_u2s(const Batch& B, uint32_t s, uint8_t* u2s, uint32_t lane, uint32_t* nin_out)
 {
-    __shared__ uint8_t u2s[4][256];
-    __shared__ uint32_t freq[4][kMaxAlpha];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t s = blockIdx.x * 4 + wave;
-    if (s >= B.nstreams || (B.flags[s] & kFlagHost)) return;
-    const uint32_t n = B.n[s];
-    const size_t o = (size_t)s * B.cap;
-    const uint8_t* T = B.T + o;
-    const uint32_t* SA = B.sa + o;
-    uint16_t* out = B.mtfv + (size_t)s * (B.cap + 1);
-    // makeMaps_e
-    uint32_t inu[8];
-    uint32_t nin = 0;
+    uint32_t inu[8], nin = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         inu[q] = B.inuse[s * 8 + q];
@@ -450,88 +526,266 @@ __global__ __launch_bounds__(256) void mtf_rle2(Batch B)
         uint32_t below = 0;
         for (uint32_t q = 0; q < (c >> 5); ++q) below += __popc(inu[q]);
         below += __popc(inu[c >> 5] & ((1u << (c & 31)) - 1u));
-        u2s[wave][c] = (uint8_t)below;
+        u2s[c] = (uint8_t)below;
     }
-    const uint32_t EOB = nin + 1;
-    for (uint32_t v = lane; v < kMaxAlpha; v += 64) freq[wave][v] = 0;
-    // yy[i] = i for i < nInUse; unused entries hold 255, which never matches
-    // (a symbol can be 255 only when all 256 are in use)
-    uint32_t yy = 0;
+    *nin_out = nin;
+}
+
+__global__ __launch_bounds__(256) void mtf_last(Batch B, uint32_t nseg_max, int32_t* __restrict__ seg_last)
+{
+    __shared__ uint8_t u2s[4][256];
+    __shared__ int32_t last[4][256];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.y, k = blockIdx.x * 4 + wave;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s];
+    const uint32_t j0 = k * kSeg;
+    if (j0 >= n) return;
+    const size_t o = (size_t)s * B.cap;
+    uint32_t nin;
+    make_u2s(B, s, u2s[wave], lane, &nin);
+    for (uint32_t c = lane; c < 256; c += 64) last[wave][c] = -1;
+    __builtin_amdgcn_wave_barrier();
+    uint8_t* llbuf = (uint8_t*)B.mtfv + o;  // the mtfv area is free until rle2
+    const uint32_t j1 = min(n, j0 + kSeg);
+    for (uint32_t j = j0 + lane; j < j1; j += 64) {
+        const uint32_t v = B.sa[o + j];
+        if ((v & kIdxMask) == 0) B.orig_ptr[s] = j;  // BZ2_blockSort: origPtr = sorted position of rotation 0
+        const uint32_t ll = u2s[wave][v >> 24];
+        llbuf[j] = (uint8_t)ll;
+        atomicMax(&last[wave][ll], (int32_t)j);
+    }
+    __builtin_amdgcn_wave_barrier();
+    int32_t* dst = seg_last + ((size_t)s * nseg_max + k) * 256;
+    for (uint32_t c = lane; c < 256; c += 64) dst[c] = last[wave][c];
+}
+
+__global__ __launch_bounds__(256) void mtf_prefix(Batch B, uint32_t nseg_max, int32_t* __restrict__ seg_last)
+{
+    const uint32_t s = blockIdx.x, c = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t nseg = (B.n[s] + kSeg - 1) / kSeg;
+    int32_t lb = -1;
+    for (uint32_t k = 0; k < nseg; ++k) {
+        int32_t* p = seg_last + ((size_t)s * nseg_max + k) * 256 + c;
+        const int32_t v = *p;
+        *p = lb;
+        lb = max(lb, v);
+    }
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// v_writelane_b32: lane `ln` of v takes the scalar x (both wave-uniform)
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t ln)
+{
+    const uint32_t xs = __builtin_amdgcn_readfirstlane(x);
+    const uint32_t ls = __builtin_amdgcn_readfirstlane(ln);
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(xs), "s"(ls) : "m0");
+    return v;
+}
+
+// pos += (pos < m) on two 16-bit positions per word (v_pk_sub_u16 clamp,
+// v_pk_min_u16, v_pk_add_u16)
+__device__ __forceinline__ uint32_t inc_below(uint32_t w, u16x2 m2)
+{
+    const u16x2 x = __builtin_bit_cast(u16x2, w);
+    const u16x2 one = {1, 1};
+    const u16x2 r = x + __builtin_elementwise_min(__builtin_elementwise_sub_sat(m2, x), one);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+// The list is kept as its inverse: pos[c] = place of symbol c.  Lane l holds
+// pos of symbols 4l .. 4l+3 as 16-bit fields (w0: 4l, 4l+1; w1: 4l+2, 4l+3).
+// A step reads pos[ll] (the MTF value m) with one readlane, then every symbol
+// in front of it moves back one place (two packed adds per lane) and ll goes
+// to place 0 (one writelane); m == 0 (43 % of the steps) costs nothing.
+__global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const int32_t* __restrict__ seg_last)
+{
+    __shared__ int32_t key[4][256];
+    __shared__ uint32_t posw[4][128];  // 256 16-bit positions per wave
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.y, k = blockIdx.x * 4 + wave;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s];
+    const uint32_t j0 = k * kSeg;
+    if (j0 >= n) return;
+    const size_t o = (size_t)s * B.cap;
+    uint32_t nin = 0;
+    for (int q = 0; q < 8; ++q) nin += __popc(B.inuse[s * 8 + q]);
+    // list order at j0: seen symbols by last position (descending), then the
+    // unseen ones by symbol index (ascending) -- key(unseen c) = -1 - c
+    const int32_t* lb = seg_last + ((size_t)s * nseg_max + k) * 256;
+    uint16_t* pos = (uint16_t*)posw[wave];
+    for (uint32_t c = lane; c < 256; c += 64) {
+        const int32_t v = c < nin ? lb[c] : INT32_MIN;
+        key[wave][c] = (c < nin && v < 0) ? -1 - (int32_t)c : v;
+        pos[c] = 0xFFFFu;  // symbols not in use: never below any m
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t c = lane; c < nin; c += 64) {
+        const int32_t kc = key[wave][c];
+        uint32_t r = 0;
+        for (uint32_t d = 0; d < nin; ++d) r += key[wave][d] > kc ? 1u : 0u;
+        pos[c] = (uint16_t)r;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t w0 = posw[wave][2 * lane], w1 = posw[wave][2 * lane + 1];
+    const uint8_t* llbuf = (const uint8_t*)B.mtfv + o;
+    uint8_t* mraw = B.uflag + o;
+    const uint32_t j1 = min(n, j0 + kSeg);
+    for (uint32_t jb = j0; jb < j1; jb += 256) {
+        // 256 symbols per round: lane l holds ll[jb + 4l .. jb + 4l + 3]
+        uint32_t llw = 0;
+        const uint32_t jl = jb + lane * 4;
+        if (jl + 3 < j1) {
+            llw = *(const uint32_t*)(llbuf + jl);  // 4-byte aligned: jb and o are multiples of 256
+        } else {
+            for (uint32_t q = 0; q < 4; ++q)
+                if (jl + q < j1) llw |= (uint32_t)llbuf[jl + q] << (8 * q);
+        }
+        const uint32_t ngrp = (min(256u, j1 - jb) + 3) >> 2;
+        uint32_t outw = 0;
+        for (uint32_t g = 0; g < ngrp; ++g) {
+            const uint32_t four = __builtin_amdgcn_readlane(llw, g);
+            uint32_t sout = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t e = lane * 4 + k;
-        yy |= (e < nin ? e : 255u) << (8 * k);
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t c = (four >> (8 * q)) & 0xFFu;
+                const uint32_t hi = c & 1u, ln = c >> 2;
+                const bool in_w1 = (c & 2u) != 0;
+                const uint32_t word = in_w1 ? __builtin_amdgcn_readlane(w1, ln) : __builtin_amdgcn_readlane(w0, ln);
+                const uint32_t m = (word >> (16 * hi)) & 0xFFFFu;
+                if (m != 0) {
+                    // the word of lane ln: c -> 0, its neighbour moves back if in front of c
+                    uint32_t other = (word >> (16 * (1 - hi))) & 0xFFFFu;
+                    other += other < m ? 1u : 0u;
+                    const uint32_t nw = hi ? other : (other << 16);
+                    const u16x2 m2 = {(unsigned short)m, (unsigned short)m};
+                    w0 = inc_below(w0, m2);
+                    w1 = inc_below(w1, m2);
+                    if (in_w1) w1 = writelane(w1, nw, ln);
+                    else w0 = writelane(w0, nw, ln);
+                }
+                sout |= (m & 0xFFu) << (8 * q);
+            }
+            outw = writelane(outw, sout, g);
+        }
+        if (jl < j1) {
+            if (jl + 3 < j1) {
+                *(uint32_t*)(mraw + jl) = outw;
+            } else {
+                for (uint32_t q = 0; q < 4; ++q)
+                    if (jl + q < j1) mraw[jl + q] = (uint8_t)(outw >> (8 * q));
+            }
+        }
     }
-    __builtin_amdgcn_wave_barrier();
-    uint32_t wr = 0, outreg = 0;
+}
+
+// zero-run digits of a run of z zeros (compress.c: z-1, then RUNA/RUNB by
+// bit, (z-2)/2 ... : bijective base 2)
+__device__ __forceinline__ uint32_t run_digits(uint32_t z)
+{
+    uint32_t d = 0;
+    uint32_t zp = z - 1;
+    while (true) {
+        ++d;
+        if (zp < 2) break;
+        zp = (zp - 2) / 2;
+    }
+    return d;
+}
+
+constexpr int kRle2Threads = 1024;
+
+__global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
+{
+    __shared__ uint32_t counts[kRle2Threads];
+    __shared__ uint32_t zsum[kRle2Threads];   // trailing zeros of the prefix (scan)
+    __shared__ uint32_t allz[kRle2Threads];   // prefix entirely zeros
+    __shared__ uint32_t freq[kMaxAlpha];
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s];
+    const size_t o = (size_t)s * B.cap;
+    const uint8_t* m = B.uflag + o;
+    uint16_t* out = B.mtfv + (size_t)s * (B.cap + 1);
+    uint32_t nin = 0;
+    for (int q = 0; q < 8; ++q) nin += __popc(B.inuse[s * 8 + q]);
+    const uint32_t EOB = nin + 1;
+    for (uint32_t v = t; v < kMaxAlpha; v += kRle2Threads) freq[v] = 0;
+    const uint32_t per = ((n + kRle2Threads - 1) / kRle2Threads + 15) & ~15u;  // 16-byte aligned chunks
+    const uint32_t c0 = min(n, t * per), c1 = min(n, c0 + per);
+    // chunk summary: trailing zeros, all-zero
+    uint32_t tz = 0;
+    bool az = true;
+    for_bytes(m + c0, c1 - c0, [&](uint32_t v) {
+        if (v == 0) ++tz;
+        else { tz = 0; az = false; }
+    });
+    zsum[t] = tz;
+    allz[t] = (c1 > c0) ? (az ? 1u : 0u) : 1u;  // empty chunks pass the carry through
+    __syncthreads();
+    // inclusive scan: (trail, all) combine: b.all ? (a.trail + b.trail, a.all) : (b.trail, false)
+    for (uint32_t off = 1; off < kRle2Threads; off <<= 1) {
+        uint32_t at = 0, aa = 1;
+        if (t >= off) { at = zsum[t - off]; aa = allz[t - off]; }
+        const uint32_t bt = zsum[t], ba = allz[t];
+        __syncthreads();
+        if (t >= off) {
+            zsum[t] = ba ? at + bt : bt;
+            allz[t] = ba & aa;
+        }
+        __syncthreads();
+    }
+    const uint32_t carry = t ? zsum[t - 1] : 0u;  // zeros pending at the chunk start
+    const uint32_t last_t = n ? (n - 1) / per : 0;
+    // pass 1: count
+    uint32_t z = carry, w = 0;
+    for_bytes(m + c0, c1 - c0, [&](uint32_t v) {
+        if (v == 0) { ++z; return; }
+        if (z) { w += run_digits(z); z = 0; }
+        ++w;
+    });
+    if (t == last_t) {
+        if (z) w += run_digits(z);
+        ++w;  // EOB
+    }
+    counts[t] = w;
+    __syncthreads();
+    for (uint32_t off = 1; off < kRle2Threads; off <<= 1) {
+        const uint32_t v = t >= off ? counts[t - off] : 0u;
+        __syncthreads();
+        counts[t] += v;
+        __syncthreads();
+    }
+    uint32_t wr = counts[t] - w;
+    // pass 2: write + frequencies
     auto emit = [&](uint32_t v) {
-        if (lane == (wr & 63)) outreg = v;
-        if (lane == 0) freq[wave][v] += 1;
-        ++wr;
-        if ((wr & 63) == 0) out[wr - 64 + lane] = (uint16_t)outreg;
+        out[wr++] = (uint16_t)v;
+        atomicAdd(&freq[v], 1u);
     };
-    uint32_t zpend = 0;
-    auto flush_zeros = [&]() {
-        if (zpend > 0) {
-            --zpend;
-            while (true) {
-                emit((zpend & 1) ? kRunB : kRunA);
-                if (zpend < 2) break;
-                zpend = (zpend - 2) / 2;
-            }
-            zpend = 0;
+    auto zeros = [&](uint32_t zz) {
+        uint32_t zp = zz - 1;
+        while (true) {
+            emit((zp & 1) ? kRunB : kRunA);
+            if (zp < 2) break;
+            zp = (zp - 2) / 2;
         }
     };
-    uint32_t orig = 0xFFFFFFFFu;  // sorted position of rotation 0 (BZ2_blockSort's origPtr)
-    for (uint32_t j0 = 0; j0 < n; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        uint32_t llv = 0;
-        if (j < n) {
-            uint32_t p = SA[j];
-            if (p == 0) orig = j;
-            p = p ? p - 1 : n - 1;
-            llv = u2s[wave][T[p]];
-        }
-        const uint32_t cnt = min(64u, n - j0);
-        for (uint32_t k = 0; k < cnt; ++k) {
-            const uint32_t ll = __builtin_amdgcn_readlane(llv, k);
-            const uint32_t y0 = __builtin_amdgcn_readfirstlane(yy) & 0xFFu;
-            if (ll == y0) {
-                ++zpend;
-                continue;
-            }
-            flush_zeros();
-            const uint32_t x = yy ^ (ll * 0x01010101u);
-            const uint32_t hz = (x - 0x01010101u) & ~x & 0x80808080u;
-            const uint64_t bl = __ballot(hz != 0);
-            const uint32_t L = (uint32_t)__builtin_ctzll(bl);
-            const uint32_t hzL = __builtin_amdgcn_readlane(hz, L);
-            const uint32_t idx = (uint32_t)__builtin_ctz(hzL) >> 3;
-            const uint32_t pos = L * 4 + idx;
-            // shift yy[0 .. pos-1] up by one, yy[0] = ll
-            uint32_t up = __shfl_up(yy, 1) >> 24;
-            if (lane == 0) up = ll;
-            const uint32_t sh = (yy << 8) | up;
-            if (lane < L) {
-                yy = sh;
-            } else if (lane == L) {
-                const uint32_t m = idx == 3 ? 0xFFFFFFFFu : ((1u << (8 * (idx + 1))) - 1u);
-                yy = (sh & m) | (yy & ~m);
-            }
-            emit(pos + 1);
-        }
+    z = carry;
+    for_bytes(m + c0, c1 - c0, [&](uint32_t v) {
+        if (v == 0) { ++z; return; }
+        if (z) { zeros(z); z = 0; }
+        emit(v + 1);
+    });
+    if (t == last_t) {
+        if (z) zeros(z);
+        emit(EOB);
     }
-    flush_zeros();
-    emit(EOB);
-    if (wr & 63) {
-        if (lane < (wr & 63)) out[(wr & ~63u) + lane] = (uint16_t)outreg;
-    }
-    __builtin_amdgcn_wave_barrier();
-    B.nmtf[s] = wr;
-    for (uint32_t v = lane; v < kMaxAlpha; v += 64) B.mtf_freq[(size_t)s * kMaxAlpha + v] = freq[wave][v];
-    const uint64_t has = __ballot(orig != 0xFFFFFFFFu);
-    const uint32_t op = __builtin_amdgcn_readlane(orig, (uint32_t)__builtin_ctzll(has));
-    if (lane == 0) B.orig_ptr[s] = op;
+    __syncthreads();
+    if (t == kRle2Threads - 1) B.nmtf[s] = counts[t];
+    for (uint32_t v = t; v < kMaxAlpha; v += kRle2Threads) B.mtf_freq[(size_t)s * kMaxAlpha + v] = freq[v];
 }
 
 // --------------------------------------------------------------- huffman --
@@ -610,6 +864,7 @@ __global__ __launch_bounds__(kHuffThreads) void huffman_tables(Batch B)
     __shared__ uint8_t len[kMaxGroups][kMaxAlpha];
     __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
     __shared__ uint32_t mfreq[kMaxAlpha];
+    __shared__ uint64_t lpack[kMaxAlpha];  // the 6 tables' lengths of a symbol, 10 bits each
     __shared__ int hb_heap[kMaxGroups][kMaxAlpha + 2];
     __shared__ int hb_weight[kMaxGroups][kMaxAlpha * 2];
     __shared__ int hb_parent[kMaxGroups][kMaxAlpha * 2];
@@ -651,18 +906,24 @@ __global__ __launch_bounds__(kHuffThreads) void huffman_tables(Batch B)
     const uint32_t nSel = (nMTF + kGSize - 1) / kGSize;
     for (int iter = 0; iter < kIters; ++iter) {
         for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rfreq[i / kMaxAlpha][i % kMaxAlpha] = 0;
+        for (int v = t; v < alphaSize; v += kHuffThreads) {
+            uint64_t lp = 0;
+            for (int q = 0; q < nGroups; ++q) lp |= (uint64_t)len[q][v] << (10 * q);
+            lpack[v] = lp;
+        }
         __syncthreads();
         for (uint32_t g = t; g < nSel; g += kHuffThreads) {
             const uint32_t gs = g * kGSize, ge = min(nMTF, gs + kGSize);
-            uint32_t cost[kMaxGroups] = {0, 0, 0, 0, 0, 0};
-            for (uint32_t i = gs; i < ge; ++i) {
-                const uint32_t v = mtfv[i];
-                for (int q = 0; q < nGroups; ++q) cost[q] += len[q][v];
-            }
+            // a group's cost under every table at once: 50 symbols x length <= 17
+            // stays below 1024 per 10-bit field (bzip2 sums UInt16 costs)
+            uint64_t acc = 0;
+            for (uint32_t i = gs; i < ge; ++i) acc += lpack[mtfv[i]];
             int bt = -1;
             uint32_t bc = 999999999u;
-            for (int q = 0; q < nGroups; ++q)
-                if ((cost[q] & 0xFFFFu) < bc) { bc = cost[q] & 0xFFFFu; bt = q; }
+            for (int q = 0; q < nGroups; ++q) {
+                const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
+                if (cq < bc) { bc = cq; bt = q; }
+            }
             sel[g] = (uint8_t)bt;
             for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
         }
@@ -924,10 +1185,11 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     const uint32_t sel_cap = (uint32_t)align_up(cap / kGSize + 8, 64);
     const size_t N = (size_t)nstreams * cap;
     size_t b = 0;
-    b += align_up((size_t)nstreams * raw_cap, 256);           // raw
+    b += align_up((size_t)nstreams * align_up(raw_cap, 16), 256);   // raw
     b += align_up(N, 256);                                      // T
     b += 2 * align_up(N * 8, 256);                              // keys
-    b += 3 * align_up(N * 4, 256);                              // vals, sa, rank
+    b += 6 * align_up(N * 4, 256);                              // vals_a, sa, rank, vals_b, cl0, cl1
+    b += align_up(N, 256);                                      // uflag
     b += align_up((size_t)nstreams * (cap + 1) * 2, 256);       // mtfv
     b += 2 * align_up((size_t)nstreams * sel_cap, 256);         // sel, sel_mtf
     b += align_up((size_t)nstreams * kMaxGroups * kMaxAlpha, 256);       // len
@@ -936,7 +1198,7 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * kMaxAlpha * 4, 256);       // mtf_freq
     b += align_up((size_t)nstreams * 8 * 4, 256);               // inuse
     b += 16 * align_up((size_t)nstreams * 4 + 64, 256);         // small per-stream arrays
-    b += align_up(((size_t)nstreams + 1) * 8, 256);             // offsets
+    b += align_up(((size_t)nstreams + 1) * 8 + 16, 256);        // offsets + counters
     return b;
 }
 
@@ -971,7 +1233,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.g.bpp = bpp;
     B.first_block = first;
     B.nstreams = count;
-    B.raw_cap = raw_cap;
+    B.raw_cap = (uint32_t)align_up(raw_cap, 16);  // stream stride of the raw blocks (16-byte loads)
     B.cap = (uint32_t)align_up((size_t)raw_cap + raw_cap / 4 + 64, 256);
     B.out_cap = (uint32_t)align_up((size_t)raw_cap + raw_cap / 50 + 4096, 256);
     B.sel_cap = (uint32_t)align_up(B.cap / kGSize + 8, 64);
@@ -982,13 +1244,17 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (N >= (1ull << 32)) return LFM_HIP_EINVAL;
     uint8_t* p = (uint8_t*)d_ws;
     auto take = [&](size_t bytes) { uint8_t* r = p; p += align_up(bytes, 256); return r; };
-    B.raw = take((size_t)count * raw_cap);
+    B.raw = take((size_t)count * B.raw_cap);
     B.T = take(N);
     B.keys_a = (uint64_t*)take(N * 8);
     B.keys_b = (uint64_t*)take(N * 8);
     B.vals_a = (uint32_t*)take(N * 4);
     B.sa = (uint32_t*)take(N * 4);
     B.rank = (uint32_t*)take(N * 4);
+    B.vals_b = (uint32_t*)take(N * 4);
+    B.cl0 = (uint32_t*)take(N * 4);
+    B.cl1 = (uint32_t*)take(N * 4);
+    B.uflag = take(N);
     B.mtfv = (uint16_t*)take((size_t)count * (B.cap + 1) * 2);
     B.sel = take((size_t)count * B.sel_cap);
     B.sel_mtf = take((size_t)count * B.sel_cap);
@@ -1001,7 +1267,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
                           &B.orig_ptr, &B.nsel, &B.ngroups, &B.out_bytes};
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
     for (int k = (int)(sizeof(small) / sizeof(small[0])); k < 16; ++k) (void)take((size_t)count * 4 + 64);
-    uint64_t* offs = (uint64_t*)take(((size_t)count + 1) * 8);
+    uint64_t* offs = (uint64_t*)take(((size_t)count + 1) * 8 + 16);
 
     hipError_t e = hipSuccess;
     auto ok = [&]() { return (e = hipGetLastError()) == hipSuccess; };
@@ -1009,39 +1275,72 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     hipLaunchKernelGGL(rle1_crc, dim3(count), dim3(kRleThreads), 0, st, B);
     hipLaunchKernelGGL(bwt_init_keys, dim3(32, count), dim3(256), 0, st, B);
     if (!ok()) return LFM_HIP_ERUNTIME;
-    // segmented radix sort temporary storage (sized for the full batch)
-    size_t tmp_bytes = 0;
-    e = rocprim::segmented_radix_sort_pairs(nullptr, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
-                                            count, B.seg_begin, B.seg_end, 0, 64, st);
-    if (e != hipSuccess) return LFM_HIP_ERUNTIME;
+    // rocPRIM temporary storage: the largest need of the primitives below
+    size_t tmp_bytes = 0, q = 0;
+    uint32_t* d_cnt = offs == nullptr ? nullptr : (uint32_t*)(offs + count + 1);  // two counters after offs
+    e = rocprim::segmented_radix_sort_pairs(nullptr, q, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N, count,
+                                            B.seg_begin, B.seg_end, 0, 64, st);
+    tmp_bytes = std::max(tmp_bytes, q);
+    e = rocprim::radix_sort_pairs(nullptr, q, B.keys_a, B.keys_b, B.vals_a, B.vals_b, (unsigned)N, 0, 52, st);
+    tmp_bytes = std::max(tmp_bytes, q);
+    e = rocprim::select(nullptr, q, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
+    tmp_bytes = std::max(tmp_bytes, q);
+    e = rocprim::inclusive_scan(nullptr, q, (uint32_t*)B.keys_a, (uint32_t*)B.keys_a + N, (size_t)N,
+                                rocprim::maximum<uint32_t>(), st);
+    tmp_bytes = std::max(tmp_bytes, q);
     void* tmp = nullptr;
     if (hipMallocAsync(&tmp, tmp_bytes, st) != hipSuccess) return LFM_HIP_ERUNTIME;
-    // round 0: the first 8 bytes; then (rank[i], rank[i+h]) for h = 8, 16, ...
+    // round 0: every rotation by its first kKeyBytes bytes (one segment per stream)
     e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N, count,
-                                            B.seg_begin, B.seg_end, 0, 64, st);
+                                            B.seg_begin, B.seg_end, 0, 8 * kKeyBytes, st);
+    if (e == hipSuccess && hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess) e = hipErrorUnknown;
     if (e == hipSuccess) {
-        uint32_t h = 8;
-        for (int round = 0; round < 32 && e == hipSuccess; ++round) {
-            hipLaunchKernelGGL(bwt_rank, dim3(count), dim3(1024), 0, st, B, h);
-            // host check of the remaining work every round (a few bytes)
-            std::vector<uint32_t> done(count);
-            if (hipMemcpyAsync(done.data(), B.done, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess) {
-                e = hipErrorUnknown;
-                break;
-            }
-            bool all = true;
-            for (uint32_t i = 0; i < count && all; ++i) all = done[i] != 0;
-            if (all) break;
-            hipLaunchKernelGGL(bwt_double_keys, dim3(32, count), dim3(256), 0, st, B, h);
-            e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
-                                                    count, B.seg_begin, B.seg_end, 0, 40, st);
-            h *= 2;
+        hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B);
+        e = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
+    }
+    // doubling rounds over the still-tied rotations only (2.4 % of them after
+    // 6 bytes on light-field symbols)
+    uint32_t* cl = B.cl0;
+    uint32_t* cl_next = B.cl1;
+    uint32_t h = kKeyBytes;
+    const uint32_t max_n = B.cap;
+    while (e == hipSuccess) {
+        uint32_t cnt = 0;
+        if (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            e = hipErrorUnknown;
+            break;
         }
+        if (cnt == 0) break;
+        if (h >= max_n) {  // every remaining tie is a pair of equal rotations
+            hipLaunchKernelGGL(bwt_flag_periodic, dim3(256), dim3(256), 0, st, B, cl, d_cnt);
+            break;
+        }
+        const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
+        hipLaunchKernelGGL(bwt_comp_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, h);
+        e = rocprim::radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.vals_b, cnt, 0, 52, st);
+        if (e != hipSuccess) break;
+        uint32_t* hv = (uint32_t*)B.keys_a;  // the sort has consumed keys_a
+        uint32_t* hvs = hv + cnt;
+        hipLaunchKernelGGL(bwt_comp_heads, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, hv);
+        e = rocprim::inclusive_scan(tmp, tmp_bytes, hv, hvs, (size_t)cnt, rocprim::maximum<uint32_t>(), st);
+        if (e != hipSuccess) break;
+        hipLaunchKernelGGL(bwt_comp_rank, dim3(grid), dim3(256), 0, st, B, d_cnt, hvs);
+        e = rocprim::select(tmp, tmp_bytes, cl, B.uflag, cl_next, d_cnt, (size_t)cnt, st);
+        std::swap(cl, cl_next);
+        h *= 2;
     }
     (void)hipFreeAsync(tmp, st);
     if (e != hipSuccess) return LFM_HIP_ERUNTIME;
-    hipLaunchKernelGGL(mtf_rle2, dim3((count + 3) / 4), dim3(256), 0, st, B);
+    {
+        const uint32_t nseg_max = (B.cap + kSeg - 1) / kSeg;
+        int32_t* seg_last = (int32_t*)B.keys_a;  // free after the BWT (count * nseg_max KiB << N * 8 bytes)
+        const dim3 g((nseg_max + 3) / 4, count);
+        hipLaunchKernelGGL(mtf_last, g, dim3(256), 0, st, B, nseg_max, seg_last);
+        hipLaunchKernelGGL(mtf_prefix, dim3(count), dim3(256), 0, st, B, nseg_max, seg_last);
+        hipLaunchKernelGGL(mtf_seg, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
+        hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
+    }
     hipLaunchKernelGGL(huffman_tables, dim3(count), dim3(kHuffThreads), 0, st, B);
     if (hipMemsetAsync(B.words, 0, (size_t)count * B.out_cap, st) != hipSuccess) return LFM_HIP_ERUNTIME;
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);

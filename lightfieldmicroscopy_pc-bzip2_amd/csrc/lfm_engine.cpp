@@ -528,11 +528,11 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     const uint32_t block_bytes = h.getBlockSizeBytes();
     const int level = std::min(9, (int)((block_bytes + 99999) / 100000));  // klb_imageIO.cpp:108
     const size_t out_cap = ((size_t)block_bytes + block_bytes / 50 + 4096 + 255) / 256 * 256;
-    // batch: bounded by a workspace budget (env LFM_BZ2_GPU_BUDGET_MB, default 24 GiB)
+    // batch: bounded by a workspace budget (env LFM_BZ2_GPU_BUDGET_MB, default 48 GiB)
     static const size_t budget = [] {
         const char* e = std::getenv("LFM_BZ2_GPU_BUDGET_MB");
         const long v = e ? std::atol(e) : 0;
-        return (size_t)(v > 0 ? v : 24 * 1024) << 20;
+        return (size_t)(v > 0 ? v : 48 * 1024) << 20;
     }();
     const size_t per_stream = lfm_hip_bzip2_workspace_bytes(1, block_bytes) + out_cap;
     uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, budget / per_stream));
