@@ -143,7 +143,8 @@ def main():
         t0 = time.perf_counter()
         k, _ = lfm.select_device(d_f0, X, Y, T, FAMILY)  # selection on the stack's frame 0
         sel_ms = (time.perf_counter() - t0) * 1e3
-        b, st = enc.encode_slab(d_img, z0, header_version=forced_request(k), nnum=T)
+        # the .lfm stays in the encoder's buffer (no copy into a Python bytes object)
+        b, st = enc.encode_slab(d_img, z0, header_version=forced_request(k), nnum=T, copy=False)
         st["select_ms"] = sel_ms
         st["total_ms"] += sel_ms
         return b, st
@@ -159,7 +160,7 @@ def main():
     for _ in range(args.steps):
         b, st = step()
         stats.append(st)
-        out_len = len(b)
+        out_len = b.nbytes
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

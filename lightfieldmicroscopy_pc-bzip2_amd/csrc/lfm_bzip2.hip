@@ -585,14 +585,15 @@ __device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t l
     return v;
 }
 
-// pos += (pos < m) on two 16-bit positions per word (v_pk_sub_u16 clamp,
-// v_pk_min_u16, v_pk_add_u16)
-__device__ __forceinline__ uint32_t inc_below(uint32_t w, u16x2 m2)
+// pos += (pos < m) on two 16-bit positions per word: sat(m - pos) is
+// non-zero exactly below m, min(., 1) turns it into the increment
+__device__ __forceinline__ uint32_t inc_below(uint32_t w, uint32_t m2)
 {
-    const u16x2 x = __builtin_bit_cast(u16x2, w);
-    const u16x2 one = {1, 1};
-    const u16x2 r = x + __builtin_elementwise_min(__builtin_elementwise_sub_sat(m2, x), one);
-    return __builtin_bit_cast(uint32_t, r);
+    uint32_t d, r;
+    asm volatile("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "s"(m2), "v"(w));
+    asm volatile("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(d) : "v"(d));
+    asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(w), "v"(d));
+    return r;
 }
 
 // The list is kept as its inverse: pos[c] = place of symbol c.  Lane l holds
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const
                     uint32_t other = (word >> (16 * (1 - hi))) & 0xFFFFu;
                     other += other < m ? 1u : 0u;
                     const uint32_t nw = hi ? other : (other << 16);
-                    const u16x2 m2 = {(unsigned short)m, (unsigned short)m};
+                    const uint32_t m2 = m | (m << 16);
                     w0 = inc_below(w0, m2);
                     w1 = inc_below(w1, m2);
                     if (in_w1) w1 = writelane(w1, nw, ln);

@@ -312,9 +312,12 @@ Encoder::~Encoder()
         if (d_sym_) (void)hipFree(d_sym_);
         if (d_ws_) (void)hipFree(d_ws_);
         if (d_prev_) (void)hipFree(d_prev_);
-        if (d_bz_ws_) (void)hipFree(d_bz_ws_);
-        if (d_bz_out_) (void)hipFree(d_bz_out_);
-        if (h_bz_out_) (void)hipHostFree(h_bz_out_);
+        for (BzSlot& sl : bz_) {
+            if (sl.d_ws) (void)hipFree(sl.d_ws);
+            if (sl.d_out) (void)hipFree(sl.d_out);
+            if (sl.h_out) (void)hipHostFree(sl.h_out);
+            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        }
         if (h_sym_) (void)hipHostFree(h_sym_);
         if (ev0_) (void)hipEventDestroy(ev0_);
         if (ev1_) (void)hipEventDestroy(ev1_);
@@ -528,64 +531,115 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     const uint32_t block_bytes = h.getBlockSizeBytes();
     const int level = std::min(9, (int)((block_bytes + 99999) / 100000));  // klb_imageIO.cpp:108
     const size_t out_cap = ((size_t)block_bytes + block_bytes / 50 + 4096 + 255) / 256 * 256;
-    // batch: bounded by a workspace budget (env LFM_BZ2_GPU_BUDGET_MB, default 48 GiB)
+    const size_t rle_cap = ((size_t)block_bytes + block_bytes / 4 + 64 + 255) / 256 * 256;
+    // Batches run in a pipeline of kBzSlots HIP streams (one host thread
+    // each): one batch's latency-bound stages (MTF, Huffman tables, the
+    // host-synchronised doubling rounds) overlap another batch's sorts.  The
+    // workspace budget (env LFM_BZ2_GPU_BUDGET_MB, default 48 GiB) is split
+    // between the slots.
     static const size_t budget = [] {
         const char* e = std::getenv("LFM_BZ2_GPU_BUDGET_MB");
         const long v = e ? std::atol(e) : 0;
         return (size_t)(v > 0 ? v : 48 * 1024) << 20;
     }();
     const size_t per_stream = lfm_hip_bzip2_workspace_bytes(1, block_bytes) + out_cap;
-    uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nblocks, budget / per_stream));
-    if (batch * ((block_bytes + block_bytes / 4 + 64 + 255) / 256 * 256) >= (1ull << 32))
-        batch = ((1ull << 32) - 1) / ((block_bytes + block_bytes / 4 + 64 + 255) / 256 * 256);
+    uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>((nblocks + kBzSlots - 1) / kBzSlots,
+                                                                budget / kBzSlots / per_stream));
+    batch = std::min<uint64_t>(batch, ((1ull << 32) - 1) / rle_cap);
+    const uint64_t nbatch = (nblocks + batch - 1) / batch;
+    const int nslots = (int)std::min<uint64_t>(kBzSlots, nbatch);
     const size_t ws = lfm_hip_bzip2_workspace_bytes((uint32_t)batch, block_bytes);
-    if (!dev_alloc(d_bz_ws_, d_bz_ws_cap_, ws)) return 3;
-    if (!dev_alloc(d_bz_out_, d_bz_out_cap_, batch * out_cap)) return 3;
-    if (!h_bz_out_ || h_bz_out_cap_ < batch * out_cap) {
-        if (h_bz_out_) (void)hipHostFree(h_bz_out_);
-        h_bz_out_ = nullptr;
-        h_bz_out_cap_ = 0;
-        if (hipHostMalloc(&h_bz_out_, batch * out_cap, hipHostMallocDefault) != hipSuccess) return 3;
-        h_bz_out_cap_ = batch * out_cap;
+    for (int k = 0; k < nslots; ++k) {
+        BzSlot& sl = bz_[k];
+        if (!sl.stream && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) return 3;
+        if (!dev_alloc(sl.d_ws, sl.d_ws_cap, ws)) return 3;
+        if (!dev_alloc(sl.d_out, sl.d_out_cap, batch * out_cap)) return 3;
+        if (!sl.h_out || sl.h_out_cap < batch * out_cap) {
+            if (sl.h_out) (void)hipHostFree(sl.h_out);
+            sl.h_out = nullptr;
+            sl.h_out_cap = 0;
+            if (hipHostMalloc(&sl.h_out, batch * out_cap, hipHostMallocDefault) != hipSuccess) return 3;
+            sl.h_out_cap = batch * out_cap;
+        }
     }
     uint32_t dims[5], bs[5];
     for (int d = 0; d < 5; ++d) {
         dims[d] = h.xyzct[d];
         bs[d] = h.blockSize[d];
     }
-    std::vector<uint64_t> sizes(batch);
-    std::vector<uint32_t> flags(batch);
+    // per batch: sizes / flags, and the ready / consumed hand-shake with the
+    // in-order writer below (slot k reuses its buffers for batch b + kBzSlots)
+    std::vector<std::vector<uint64_t>> sizes(nbatch);
+    std::vector<std::vector<uint32_t>> flags(nbatch);
+    std::vector<int> state(nbatch, 0);  // 0 pending, 1 ready, 2 consumed, -1 failed
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<bool> abort_all{false};
+    std::vector<double> d2h(nslots, 0.0);
+    auto worker = [&](int k) {
+        (void)hipSetDevice(device_);
+        BzSlot& sl = bz_[k];
+        for (uint64_t b = k; b < nbatch; b += nslots) {
+            if (b >= (uint64_t)nslots) {  // wait until the writer consumed batch b - nslots
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return state[b - nslots] != 1 || abort_all.load(); });
+                if (abort_all.load() || state[b - nslots] < 0) break;
+            }
+            const uint64_t b0 = b * batch;
+            const uint32_t cnt = (uint32_t)std::min<uint64_t>(batch, nblocks - b0);
+            sizes[b].assign(cnt, 0);
+            flags[b].assign(cnt, 0);
+            int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
+                                          ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
+            if (ok) {
+                uint64_t tot = 0;
+                for (uint32_t i = 0; i < cnt; ++i) tot += sizes[b][i];
+                auto t0 = clk::now();
+                ok = hipMemcpyAsync(sl.h_out, sl.d_out, tot, hipMemcpyDeviceToHost, sl.stream) == hipSuccess &&
+                     hipStreamSynchronize(sl.stream) == hipSuccess;
+                d2h[k] += ms_since(t0);
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                state[b] = ok ? 1 : -1;
+            }
+            cv.notify_all();
+            if (!ok) break;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int k = 0; k < nslots; ++k) pool.emplace_back(worker, k);
+
     const uint8_t* h_all = nullptr;  // host copy of the symbols, only if a stream needs the host library
     std::vector<uint8_t> in(block_bytes), out((size_t)std::ceil((float)block_bytes * 2.0f + 50.0f));
     int rc = sink.begin(h);
     uint64_t offset = 0;
-    for (uint64_t b0 = 0; b0 < nblocks && !rc; b0 += batch) {
-        const uint32_t cnt = (uint32_t)std::min<uint64_t>(batch, nblocks - b0);
-        if (lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, d_bz_ws_, ws,
-                                 d_bz_out_, sizes.data(), flags.data(), stream_) != LFM_HIP_OK)
-            return 3;
-        uint64_t tot = 0;
-        for (uint32_t i = 0; i < cnt; ++i) tot += sizes[i];
-        auto t0 = clk::now();
-        if (hipMemcpyAsync(h_bz_out_, d_bz_out_, tot, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
-            hipStreamSynchronize(stream_) != hipSuccess)
-            return 3;
-        if (st) st->d2h_ms += ms_since(t0);
-        const uint8_t* p = (const uint8_t*)h_bz_out_;
+    for (uint64_t b = 0; b < nbatch && !rc; ++b) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return state[b] != 0; });
+            if (state[b] < 0) rc = 3;
+        }
+        if (rc) break;
+        const uint64_t b0 = b * batch;
+        const uint32_t cnt = (uint32_t)sizes[b].size();
+        const uint8_t* p = (const uint8_t*)bz_[b % nslots].h_out;
         for (uint32_t i = 0; i < cnt && !rc; ++i) {
-            if (flags[i]) {
+            if (flags[b][i]) {
                 if (!h_all) {
                     const size_t bytes = h.getImageSizeBytes();
                     if (!h_sym_ || h_sym_cap_ < bytes) {
                         if (h_sym_) (void)hipHostFree(h_sym_);
                         h_sym_ = nullptr;
                         h_sym_cap_ = 0;
-                        if (hipHostMalloc(&h_sym_, bytes, hipHostMallocDefault) != hipSuccess) return 3;
+                        if (hipHostMalloc(&h_sym_, bytes, hipHostMallocDefault) != hipSuccess) { rc = 3; break; }
                         h_sym_cap_ = bytes;
                     }
                     if (hipMemcpyAsync(h_sym_, d_sym, bytes, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
-                        hipStreamSynchronize(stream_) != hipSuccess)
-                        return 3;
+                        hipStreamSynchronize(stream_) != hipSuccess) {
+                        rc = 3;
+                        break;
+                    }
                     h_all = (const uint8_t*)h_sym_;
                 }
                 size_t n = 0;
@@ -595,13 +649,27 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                 if (!rc) rc = sink.append(out.data(), len);
                 offset += len;
             } else {
-                rc = sink.append(p, sizes[i]);
-                p += sizes[i];
-                offset += sizes[i];
+                rc = sink.append(p, sizes[b][i]);
+                p += sizes[b][i];
+                offset += sizes[b][i];
             }
             h.blockOffset[b0 + i] = offset;
         }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            state[b] = 2;
+            if (rc) abort_all = true;
+        }
+        cv.notify_all();
     }
+    if (rc) {
+        std::lock_guard<std::mutex> lk(mu);
+        abort_all = true;
+    }
+    cv.notify_all();
+    for (auto& t : pool) t.join();
+    if (st)
+        for (double v : d2h) st->d2h_ms += v;
     if (rc) return rc;
     return sink.finish(h);
 }

@@ -98,9 +98,15 @@ private:
     void* d_sym_ = nullptr; size_t d_sym_cap_ = 0;
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
     void* d_prev_ = nullptr; size_t d_prev_cap_ = 0;
-    void* d_bz_ws_ = nullptr; size_t d_bz_ws_cap_ = 0;
-    void* d_bz_out_ = nullptr; size_t d_bz_out_cap_ = 0;
-    void* h_bz_out_ = nullptr; size_t h_bz_out_cap_ = 0;  // pinned
+    // GPU bzip2 pipeline slots (stream, workspace, device + pinned output)
+    static constexpr int kBzSlots = 2;
+    struct BzSlot {
+        hipStream_t stream = nullptr;
+        void* d_ws = nullptr; size_t d_ws_cap = 0;
+        void* d_out = nullptr; size_t d_out_cap = 0;
+        void* h_out = nullptr; size_t h_out_cap = 0;
+    };
+    BzSlot bz_[kBzSlots];
     void* h_sym_ = nullptr; size_t h_sym_cap_ = 0;   // pinned
 };
 

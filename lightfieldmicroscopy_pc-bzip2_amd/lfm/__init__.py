@@ -260,9 +260,10 @@ class Encoder:
         return img.ctypes.data, 0, xyzct, data_type, img
 
     def encode(self, img, header_version=0, nnum=13, block_size=None, compression=1, metadata=None,
-               xyzct=None, data_type=None):
+               xyzct=None, data_type=None, copy=True):
         """img: numpy array [t,c,z,y,x] (host) or a torch CUDA tensor (device, uint16 viewed as int16 ok).
-        Returns (bytes, stats dict)."""
+        Returns (.lfm, stats dict): bytes, or with copy=False a zero-copy
+        memoryview of the encoder's buffer, valid until its next call."""
         ptr, dev, xyzct, data_type, keep = self._operand(img, xyzct, data_type)
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_uint64()
@@ -272,10 +273,12 @@ class Encoder:
                                       _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
         _check(rc, "lfm_encoder_encode")
         del keep
+        if not copy:
+            return memoryview((ctypes.c_uint8 * n.value).from_address(ctypes.addressof(out.contents))), st.as_dict()
         return ctypes.string_at(out, n.value), st.as_dict()
 
     def encode_slab(self, img, z0, prev=None, header_version=8, nnum=13, block_size=None, compression=1,
-                    metadata=None, xyzct=None, data_type=None):
+                    metadata=None, xyzct=None, data_type=None, copy=True):
         """Encode the z-slab of a larger stack that starts at global frame z0
         (see lfm_encoder_encode_slab); prev = raw frame z0-1 (same residency
         as img), needed when the slab starts at an odd frame of a video stack.
@@ -295,6 +298,8 @@ class Encoder:
                                            _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
         _check(rc, "lfm_encoder_encode_slab")
         del keep
+        if not copy:
+            return memoryview((ctypes.c_uint8 * n.value).from_address(ctypes.addressof(out.contents))), st.as_dict()
         return ctypes.string_at(out, n.value), st.as_dict()
 
 
