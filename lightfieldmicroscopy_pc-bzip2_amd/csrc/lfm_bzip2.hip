@@ -44,6 +44,7 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -114,6 +115,7 @@ struct Batch {
     uint32_t* ngroups;
     uint8_t* len;            // kMaxGroups * kMaxAlpha per stream
     uint32_t* code;          // kMaxGroups * kMaxAlpha per stream
+    uint32_t* rfreq;         // kMaxGroups * kMaxAlpha per stream
     uint32_t* words;         // out_cap / 4 per stream, MSB-first bit words
     uint32_t* out_bytes;
 };
@@ -394,11 +396,72 @@ __global__ __launch_bounds__(256) void bwt_init_keys(Batch B)
     }
 }
 
-// After the first sort (keys_b = 6-byte prefixes, sa): rank[sa[j]] = first
+// Global first round: every stream's rotations in one radix sort with the
+// stream index above the 6-byte prefix (one device-wide sort runs at HBM
+// speed; a segmented sort walks each 150k-element segment with one
+// workgroup).  soff = exclusive offsets of the stream lengths.
+__global__ __launch_bounds__(1024) void bwt_stream_offsets(Batch B, uint32_t* __restrict__ soff)
+{
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, ns = B.nstreams;
+    const uint32_t per = (ns + 1023) / 1024;
+    const uint32_t s0 = min(ns, t * per), s1 = min(ns, s0 + per);
+    uint32_t sum = 0;
+    for (uint32_t s = s0; s < s1; ++s) sum += (B.flags[s] & kFlagHost) ? 0u : B.n[s];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t acc = part[t] - sum;
+    for (uint32_t s = s0; s < s1; ++s) {
+        soff[s] = acc;
+        acc += (B.flags[s] & kFlagHost) ? 0u : B.n[s];
+    }
+    if (t == 1023) soff[ns] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void bwt_init_keys_global(Batch B, const uint32_t* __restrict__ soff)
+{
+    const uint32_t s = blockIdx.y;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
+    const uint32_t base = soff[s];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        uint64_t k = 0;
+        uint32_t j = i;
+#pragma unroll
+        for (uint32_t q = 0; q < kKeyBytes; ++q) {
+            k = (k << 8) | T[j];
+            j = j + 1 == n ? 0 : j + 1;
+        }
+        B.keys_a[base + i] = ((uint64_t)s << (8 * kKeyBytes)) | k;
+        B.vals_a[base + i] = i | ((uint32_t)T[i ? i - 1 : n - 1] << 24);
+    }
+}
+
+// sorted global order -> per-stream slots (the stream index is the key's top)
+__global__ __launch_bounds__(256) void bwt_scatter_global(Batch B, const uint32_t* __restrict__ soff,
+                                                          uint32_t total)
+{
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
+        const uint64_t k = B.keys_b[g];
+        const uint32_t s = (uint32_t)(k >> (8 * kKeyBytes));
+        const size_t slot = (size_t)s * B.cap + (g - soff[s]);
+        B.keys_a[slot] = k;
+        B.sa[slot] = B.vals_b[g];
+    }
+}
+
+// After the first sort (6-byte prefixes, sa): rank[sa[j]] = first
 // sorted position of j's group, uflag[slot] = 1 where j's group has more than
 // one rotation.  Tiles of 1024 consecutive positions keep every load
 // coalesced; the group start is a running max carried across tiles.
-__global__ __launch_bounds__(1024) void bwt_rank0(Batch B)
+__global__ __launch_bounds__(1024) void bwt_rank0(Batch B, const uint64_t* __restrict__ keys)
 {
     __shared__ uint32_t wmax[16];
     __shared__ uint32_t carry;
@@ -406,7 +469,7 @@ __global__ __launch_bounds__(1024) void bwt_rank0(Batch B)
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
     const size_t o = (size_t)s * B.cap;
-    const uint64_t* K = B.keys_b + o;
+    const uint64_t* K = keys + o;
     const uint32_t* SA = B.sa + o;
     if (t == 0) carry = 0;
     __syncthreads();
@@ -860,84 +923,126 @@ __device__ void make_code_lengths(uint8_t* len, const uint32_t* freq, int alphaS
 
 constexpr int kHuffThreads = 256;
 
-__global__ __launch_bounds__(kHuffThreads) void huffman_tables(Batch B)
+// sendMTFValues split across launches so the sequential part (the heap of
+// BZ2_hbMakeCodeLengths) runs one table per wave, many tables per CU:
+//   huff_init     nGroups and the initial partition (len 0 / 15)
+//   huff_select   x4: selector per 50 symbols (first minimum cost, all tables
+//                 summed at once in 10-bit fields), then symbol frequencies
+//                 per selected table
+//   huff_lengths  x4: BZ2_hbMakeCodeLengths, one wave per (stream, table)
+//   huff_final    selector MTF and the codes (BZ2_hbAssignCodes)
+__device__ __forceinline__ uint32_t stream_nin(const Batch& B, uint32_t s)
 {
-    __shared__ uint8_t len[kMaxGroups][kMaxAlpha];
-    __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
-    __shared__ uint32_t mfreq[kMaxAlpha];
-    __shared__ uint64_t lpack[kMaxAlpha];  // the 6 tables' lengths of a symbol, 10 bits each
-    __shared__ int hb_heap[kMaxGroups][kMaxAlpha + 2];
-    __shared__ int hb_weight[kMaxGroups][kMaxAlpha * 2];
-    __shared__ int hb_parent[kMaxGroups][kMaxAlpha * 2];
-    __shared__ int s_ngroups;
+    uint32_t nin = 0;
+    for (int q = 0; q < 8; ++q) nin += __popc(B.inuse[s * 8 + q]);
+    return nin;
+}
+
+__global__ __launch_bounds__(64) void huff_init(Batch B)
+{
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t nMTF = B.nmtf[s];
-    uint32_t nin = 0;
-    for (int q = 0; q < 8; ++q) nin += __popc(B.inuse[s * 8 + q]);
-    const int alphaSize = (int)nin + 2;
+    const int alphaSize = (int)stream_nin(B, s) + 2;
+    const uint32_t* mfreq = B.mtf_freq + (size_t)s * kMaxAlpha;
+    uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
+    if (t != 0) return;
+    const int nGroups = nMTF < 200 ? 2 : nMTF < 600 ? 3 : nMTF < 1200 ? 4 : nMTF < 2400 ? 5 : 6;
+    for (int i = 0; i < kMaxGroups * kMaxAlpha; ++i) len[i] = 15;
+    int nPart = nGroups, remF = (int)nMTF, gs = 0;
+    while (nPart > 0) {
+        const int tFreq = remF / nPart;
+        int ge = gs - 1, aFreq = 0;
+        while (aFreq < tFreq && ge < alphaSize - 1) {
+            ++ge;
+            aFreq += (int)mfreq[ge];
+        }
+        if (ge > gs && nPart != nGroups && nPart != 1 && ((nGroups - nPart) % 2 == 1)) {
+            aFreq -= (int)mfreq[ge];
+            --ge;
+        }
+        for (int v = 0; v < alphaSize; ++v) len[(nPart - 1) * kMaxAlpha + v] = (v >= gs && v <= ge) ? 0 : 15;
+        --nPart;
+        gs = ge + 1;
+        remF -= aFreq;
+    }
+    B.ngroups[s] = (uint32_t)nGroups;
+    B.nsel[s] = (nMTF + kGSize - 1) / kGSize;
+}
+
+__global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
+{
+    __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
+    __shared__ uint64_t lpack[kMaxAlpha];  // the tables' lengths of a symbol, 10 bits each
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t nMTF = B.nmtf[s], nSel = B.nsel[s];
+    const int nGroups = (int)B.ngroups[s];
+    const int alphaSize = (int)stream_nin(B, s) + 2;
+    const uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
     const uint16_t* mtfv = B.mtfv + (size_t)s * (B.cap + 1);
     uint8_t* sel = B.sel + (size_t)s * B.sel_cap;
-    for (int v = t; v < kMaxAlpha; v += kHuffThreads) mfreq[v] = B.mtf_freq[(size_t)s * kMaxAlpha + v];
-    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) len[i / kMaxAlpha][i % kMaxAlpha] = 15;
-    __syncthreads();
-    if (t == 0) {
-        int nGroups = nMTF < 200 ? 2 : nMTF < 600 ? 3 : nMTF < 1200 ? 4 : nMTF < 2400 ? 5 : 6;
-        s_ngroups = nGroups;
-        int nPart = nGroups, remF = (int)nMTF, gs = 0;
-        while (nPart > 0) {
-            const int tFreq = remF / nPart;
-            int ge = gs - 1, aFreq = 0;
-            while (aFreq < tFreq && ge < alphaSize - 1) {
-                ++ge;
-                aFreq += (int)mfreq[ge];
-            }
-            if (ge > gs && nPart != nGroups && nPart != 1 && ((nGroups - nPart) % 2 == 1)) {
-                aFreq -= (int)mfreq[ge];
-                --ge;
-            }
-            for (int v = 0; v < alphaSize; ++v) len[nPart - 1][v] = (v >= gs && v <= ge) ? 0 : 15;
-            --nPart;
-            gs = ge + 1;
-            remF -= aFreq;
-        }
+    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rfreq[i / kMaxAlpha][i % kMaxAlpha] = 0;
+    for (int v = t; v < alphaSize; v += kHuffThreads) {
+        uint64_t lp = 0;
+        for (int q = 0; q < nGroups; ++q) lp |= (uint64_t)len[q * kMaxAlpha + v] << (10 * q);
+        lpack[v] = lp;
     }
     __syncthreads();
-    const int nGroups = s_ngroups;
-    const uint32_t nSel = (nMTF + kGSize - 1) / kGSize;
-    for (int iter = 0; iter < kIters; ++iter) {
-        for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rfreq[i / kMaxAlpha][i % kMaxAlpha] = 0;
-        for (int v = t; v < alphaSize; v += kHuffThreads) {
-            uint64_t lp = 0;
-            for (int q = 0; q < nGroups; ++q) lp |= (uint64_t)len[q][v] << (10 * q);
-            lpack[v] = lp;
+    for (uint32_t g = t; g < nSel; g += kHuffThreads) {
+        const uint32_t gs = g * kGSize, ge = min(nMTF, gs + kGSize);
+        // a group's cost under every table at once: 50 symbols x length <= 17
+        // stays below 1024 per 10-bit field (bzip2 sums UInt16 costs)
+        uint64_t acc = 0;
+        for (uint32_t i = gs; i < ge; ++i) acc += lpack[mtfv[i]];
+        int bt = -1;
+        uint32_t bc = 999999999u;
+        for (int q = 0; q < nGroups; ++q) {
+            const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
+            if (cq < bc) { bc = cq; bt = q; }
         }
-        __syncthreads();
-        for (uint32_t g = t; g < nSel; g += kHuffThreads) {
-            const uint32_t gs = g * kGSize, ge = min(nMTF, gs + kGSize);
-            // a group's cost under every table at once: 50 symbols x length <= 17
-            // stays below 1024 per 10-bit field (bzip2 sums UInt16 costs)
-            uint64_t acc = 0;
-            for (uint32_t i = gs; i < ge; ++i) acc += lpack[mtfv[i]];
-            int bt = -1;
-            uint32_t bc = 999999999u;
-            for (int q = 0; q < nGroups; ++q) {
-                const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
-                if (cq < bc) { bc = cq; bt = q; }
-            }
-            sel[g] = (uint8_t)bt;
-            for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
-        }
-        __syncthreads();
-        if (t < (uint32_t)nGroups)
-            make_code_lengths(len[t], rfreq[t], alphaSize, 17, hb_heap[t], hb_weight[t], hb_parent[t]);
-        __syncthreads();
+        sel[g] = (uint8_t)bt;
+        for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
     }
-    // selector MTF
-    if (t == 0) {
+    __syncthreads();
+    uint32_t* rf = B.rfreq + (size_t)s * kMaxGroups * kMaxAlpha;
+    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rf[i] = rfreq[i / kMaxAlpha][i % kMaxAlpha];
+}
+
+__global__ __launch_bounds__(256) void huff_lengths(Batch B)
+{
+    __shared__ int hb_heap[4][kMaxAlpha + 2];
+    __shared__ int hb_weight[4][kMaxAlpha * 2];
+    __shared__ int hb_parent[4][kMaxAlpha * 2];
+    __shared__ uint32_t fr[4][kMaxAlpha];
+    __shared__ uint8_t ln[4][kMaxAlpha + 2];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t task = blockIdx.x * 4 + wave;
+    const uint32_t s = task / kMaxGroups, tb = task % kMaxGroups;
+    if (s >= B.nstreams || (B.flags[s] & kFlagHost) || tb >= B.ngroups[s]) return;
+    const int alphaSize = (int)stream_nin(B, s) + 2;
+    const uint32_t* rf = B.rfreq + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
+    for (int v = lane; v < alphaSize; v += 64) fr[wave][v] = rf[v];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) make_code_lengths(ln[wave], fr[wave], alphaSize, 17, hb_heap[wave], hb_weight[wave], hb_parent[wave]);
+    __builtin_amdgcn_wave_barrier();
+    uint8_t* len = B.len + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
+    for (int v = lane; v < alphaSize; v += 64) len[v] = ln[wave][v];
+}
+
+__global__ __launch_bounds__(64) void huff_final(Batch B)
+{
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const int nGroups = (int)B.ngroups[s];
+    const uint32_t nSel = B.nsel[s];
+    const int alphaSize = (int)stream_nin(B, s) + 2;
+    const uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
+    if (t == 0) {  // selector MTF
+        const uint8_t* sel = B.sel + (size_t)s * B.sel_cap;
+        uint8_t* sm = B.sel_mtf + (size_t)s * B.sel_cap;
         uint8_t pos[kMaxGroups];
         for (int i = 0; i < nGroups; ++i) pos[i] = (uint8_t)i;
-        uint8_t* sm = B.sel_mtf + (size_t)s * B.sel_cap;
         for (uint32_t i = 0; i < nSel; ++i) {
             const uint8_t ll = sel[i];
             int j = 0;
@@ -951,26 +1056,22 @@ __global__ __launch_bounds__(kHuffThreads) void huffman_tables(Batch B)
             pos[0] = tmp;
             sm[i] = (uint8_t)j;
         }
-        B.nsel[s] = nSel;
-        B.ngroups[s] = (uint32_t)nGroups;
-    }
-    // codes (huffman.c BZ2_hbAssignCodes)
-    if (t < (uint32_t)nGroups) {
+    } else if (t <= (uint32_t)nGroups) {  // codes of table t - 1 (huffman.c BZ2_hbAssignCodes)
+        const int q = (int)t - 1;
+        const uint8_t* lq = len + q * kMaxAlpha;
         int minLen = 32, maxLen = 0;
         for (int i = 0; i < alphaSize; ++i) {
-            minLen = min(minLen, (int)len[t][i]);
-            maxLen = max(maxLen, (int)len[t][i]);
+            minLen = min(minLen, (int)lq[i]);
+            maxLen = max(maxLen, (int)lq[i]);
         }
-        uint32_t* code = B.code + ((size_t)s * kMaxGroups + t) * kMaxAlpha;
+        uint32_t* code = B.code + ((size_t)s * kMaxGroups + q) * kMaxAlpha;
         int vec = 0;
         for (int nl = minLen; nl <= maxLen; ++nl) {
             for (int i = 0; i < alphaSize; ++i)
-                if (len[t][i] == nl) code[i] = (uint32_t)vec++;
+                if (lq[i] == nl) code[i] = (uint32_t)vec++;
             vec <<= 1;
         }
     }
-    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads)
-        B.len[(size_t)s * kMaxGroups * kMaxAlpha + i] = len[i / kMaxAlpha][i % kMaxAlpha];
 }
 
 // ------------------------------------------------------------------ emit --
@@ -1162,22 +1263,31 @@ void ensure_crc_table()
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-struct Ctx {
-    int device = -1;
-    size_t cap_bytes = 0;
-    void* mem = nullptr;
-    size_t sort_tmp_bytes = 0;
-    void* sort_tmp = nullptr;
-    bool crc_uploaded = false;
-};
-
-thread_local Ctx* g_ctx = nullptr;
+// rocPRIM temporary storage for the largest use of each primitive in a batch
+// of `count` streams (size queries only: no device work).  Carved out of the
+// caller's workspace: a per-call stream-ordered allocation of these
+// gigabyte-sized buffers stalled every stream of the device for ~0.3 s.
+size_t prim_tmp_bytes(uint32_t count, uint32_t cap)
+{
+    const size_t N = (size_t)count * cap;
+    uint64_t* k = nullptr;
+    uint32_t* v = nullptr;
+    uint8_t* f = nullptr;
+    size_t tmp = 0, q = 0;
+    (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, count, v, v, 0, 64);
+    tmp = std::max(tmp, q);
+    (void)rocprim::radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, 0, 64);
+    tmp = std::max(tmp, q);
+    (void)rocprim::select(nullptr, q, rocprim::counting_iterator<uint32_t>(0), f, v, v, N);
+    tmp = std::max(tmp, q);
+    (void)rocprim::select(nullptr, q, v, f, v, v, N);
+    tmp = std::max(tmp, q);
+    (void)rocprim::inclusive_scan(nullptr, q, v, v, N, rocprim::maximum<uint32_t>());
+    tmp = std::max(tmp, q);
+    return tmp;
+}
 
 } // namespace
-
-struct lfm_bz2_ctx {
-    Ctx c;
-};
 
 extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_cap)
 {
@@ -1194,12 +1304,13 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * (cap + 1) * 2, 256);       // mtfv
     b += 2 * align_up((size_t)nstreams * sel_cap, 256);         // sel, sel_mtf
     b += align_up((size_t)nstreams * kMaxGroups * kMaxAlpha, 256);       // len
-    b += align_up((size_t)nstreams * kMaxGroups * kMaxAlpha * 4, 256);   // code
+    b += 2 * align_up((size_t)nstreams * kMaxGroups * kMaxAlpha * 4, 256);   // code, rfreq
     b += align_up((size_t)nstreams * out_cap, 256);             // words
     b += align_up((size_t)nstreams * kMaxAlpha * 4, 256);       // mtf_freq
     b += align_up((size_t)nstreams * 8 * 4, 256);               // inuse
     b += 16 * align_up((size_t)nstreams * 4 + 64, 256);         // small per-stream arrays
     b += align_up(((size_t)nstreams + 1) * 8 + 16, 256);        // offsets + counters
+    b += align_up(prim_tmp_bytes(nstreams, cap), 256);          // rocPRIM temporary storage
     return b;
 }
 
@@ -1261,6 +1372,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.sel_mtf = take((size_t)count * B.sel_cap);
     B.len = take((size_t)count * kMaxGroups * kMaxAlpha);
     B.code = (uint32_t*)take((size_t)count * kMaxGroups * kMaxAlpha * 4);
+    B.rfreq = (uint32_t*)take((size_t)count * kMaxGroups * kMaxAlpha * 4);
     B.words = (uint32_t*)take((size_t)count * B.out_cap);
     B.mtf_freq = (uint32_t*)take((size_t)count * kMaxAlpha * 4);
     B.inuse = (uint32_t*)take((size_t)count * 8 * 4);
@@ -1269,34 +1381,47 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
     for (int k = (int)(sizeof(small) / sizeof(small[0])); k < 16; ++k) (void)take((size_t)count * 4 + 64);
     uint64_t* offs = (uint64_t*)take(((size_t)count + 1) * 8 + 16);
+    size_t tmp_bytes = prim_tmp_bytes(count, B.cap);
+    void* tmp = take(tmp_bytes);
 
     hipError_t e = hipSuccess;
     auto ok = [&]() { return (e = hipGetLastError()) == hipSuccess; };
     hipLaunchKernelGGL(gather_blocks, dim3(64, count), dim3(256), 0, st, B);
     hipLaunchKernelGGL(rle1_crc, dim3(count), dim3(kRleThreads), 0, st, B);
-    hipLaunchKernelGGL(bwt_init_keys, dim3(32, count), dim3(256), 0, st, B);
+    if (std::getenv("LFM_BZ2_SORT") && std::strcmp(std::getenv("LFM_BZ2_SORT"), "segmented") == 0)
+        hipLaunchKernelGGL(bwt_init_keys, dim3(32, count), dim3(256), 0, st, B);
     if (!ok()) return LFM_HIP_ERUNTIME;
-    // rocPRIM temporary storage: the largest need of the primitives below
-    size_t tmp_bytes = 0, q = 0;
-    uint32_t* d_cnt = offs == nullptr ? nullptr : (uint32_t*)(offs + count + 1);  // two counters after offs
-    e = rocprim::segmented_radix_sort_pairs(nullptr, q, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N, count,
-                                            B.seg_begin, B.seg_end, 0, 64, st);
-    tmp_bytes = std::max(tmp_bytes, q);
-    e = rocprim::radix_sort_pairs(nullptr, q, B.keys_a, B.keys_b, B.vals_a, B.vals_b, (unsigned)N, 0, 52, st);
-    tmp_bytes = std::max(tmp_bytes, q);
-    e = rocprim::select(nullptr, q, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
-    tmp_bytes = std::max(tmp_bytes, q);
-    e = rocprim::inclusive_scan(nullptr, q, (uint32_t*)B.keys_a, (uint32_t*)B.keys_a + N, (size_t)N,
-                                rocprim::maximum<uint32_t>(), st);
-    tmp_bytes = std::max(tmp_bytes, q);
-    void* tmp = nullptr;
-    if (hipMallocAsync(&tmp, tmp_bytes, st) != hipSuccess) return LFM_HIP_ERUNTIME;
-    // round 0: every rotation by its first kKeyBytes bytes (one segment per stream)
-    e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N, count,
-                                            B.seg_begin, B.seg_end, 0, 8 * kKeyBytes, st);
+    uint32_t* d_cnt = (uint32_t*)(offs + count + 1);  // two counters after offs
+    // round 0: every rotation by its first kKeyBytes bytes
+    static const bool segmented = [] {
+        const char* v = std::getenv("LFM_BZ2_SORT");
+        return v && std::strcmp(v, "segmented") == 0;
+    }();
+    const uint64_t* rank0_keys = B.keys_b;
+    if (segmented) {  // one segment per stream
+        e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
+                                                count, B.seg_begin, B.seg_end, 0, 8 * kKeyBytes, st);
+    } else {  // all streams in one sort, stream index above the prefix
+        uint32_t* soff = B.cl1;  // free until the doubling rounds
+        hipLaunchKernelGGL(bwt_stream_offsets, dim3(1), dim3(1024), 0, st, B, soff);
+        hipLaunchKernelGGL(bwt_init_keys_global, dim3(32, count), dim3(256), 0, st, B, soff);
+        uint32_t total = 0;
+        if (hipMemcpyAsync(&total, soff + count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            e = hipErrorUnknown;
+        unsigned sbits = 1;
+        while ((1u << sbits) < count) ++sbits;
+        if (e == hipSuccess && total)
+            e = rocprim::radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.vals_b, total, 0,
+                                          8 * kKeyBytes + sbits, st);
+        if (e == hipSuccess && total)
+            hipLaunchKernelGGL(bwt_scatter_global, dim3(std::min<uint32_t>(8192, (total + 255) / 256)), dim3(256), 0,
+                               st, B, (const uint32_t*)soff, total);
+        rank0_keys = B.keys_a;
+    }
     if (e == hipSuccess && hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess) e = hipErrorUnknown;
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B);
+        hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B, rank0_keys);
         e = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
     }
     // doubling rounds over the still-tied rotations only (2.4 % of them after
@@ -1331,7 +1456,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         std::swap(cl, cl_next);
         h *= 2;
     }
-    (void)hipFreeAsync(tmp, st);
     if (e != hipSuccess) return LFM_HIP_ERUNTIME;
     {
         const uint32_t nseg_max = (B.cap + kSeg - 1) / kSeg;
@@ -1342,7 +1466,12 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         hipLaunchKernelGGL(mtf_seg, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
         hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
     }
-    hipLaunchKernelGGL(huffman_tables, dim3(count), dim3(kHuffThreads), 0, st, B);
+    hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
+    for (int it = 0; it < kIters; ++it) {
+        hipLaunchKernelGGL(huff_select, dim3(count), dim3(kHuffThreads), 0, st, B);
+        hipLaunchKernelGGL(huff_lengths, dim3((count * kMaxGroups + 3) / 4), dim3(256), 0, st, B);
+    }
+    hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
     if (hipMemsetAsync(B.words, 0, (size_t)count * B.out_cap, st) != hipSuccess) return LFM_HIP_ERUNTIME;
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(64), 0, st, B.out_bytes, count, offs);
