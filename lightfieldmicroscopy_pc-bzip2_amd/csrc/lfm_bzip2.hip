@@ -501,6 +501,117 @@ __global__ __launch_bounds__(1024) void bwt_rank0(Batch B, const uint64_t* __res
     }
 }
 
+// Tie resolution by more text.  After the first sort only the rotations in
+// a group of equal 6-byte prefixes are still unordered (2.4 % on light-field
+// symbols, 0.01 % after 11 bytes): they are re-sorted inside their groups by
+// the next 5 bytes of text, kTextRounds times, without the inverse suffix
+// array (a random 4-byte scatter per rotation) that prefix doubling needs.
+// Only ties that survive those rounds (long repeats) fall back to doubling.
+constexpr int kTextRounds = 3;
+constexpr uint32_t kTextBytes = 5;
+
+__global__ __launch_bounds__(256) void bwt_ties0(Batch B, const uint64_t* __restrict__ K, size_t N)
+{
+    for (size_t slot = blockIdx.x * (size_t)blockDim.x + threadIdx.x; slot < N;
+         slot += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(slot / B.cap);
+        const uint32_t j = (uint32_t)(slot - (size_t)s * B.cap);
+        const uint32_t n = (B.flags[s] & kFlagHost) ? 0u : B.n[s];
+        uint8_t f = 0;
+        if (j < n) {
+            const uint64_t k = K[slot];
+            f = ((j > 0 && K[slot - 1] == k) || (j + 1 < n && K[slot + 1] == k)) ? 1 : 0;
+        }
+        B.uflag[slot] = f;
+    }
+}
+
+__global__ __launch_bounds__(256) void text_gather_keys(const uint32_t* __restrict__ cl, const uint32_t* __restrict__ cnt_p,
+                                                        const uint64_t* __restrict__ K, uint64_t* __restrict__ gk)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) gk[c] = K[cl[c]];
+}
+
+// group starts of the tied list (equal keys, same stream)
+__global__ __launch_bounds__(256) void text_bounds(Batch B, const uint32_t* __restrict__ cl,
+                                                   const uint32_t* __restrict__ cnt_p, const uint64_t* __restrict__ gk,
+                                                   uint32_t* __restrict__ bnd)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x)
+        bnd[c] = (c == 0 || gk[c] != gk[c - 1] || cl[c] / B.cap != cl[c - 1] / B.cap) ? 1u : 0u;
+}
+
+// key = (group index, next kTextBytes of the rotation at offset `off`)
+__global__ __launch_bounds__(256) void text_keys(Batch B, const uint32_t* __restrict__ cl,
+                                                 const uint32_t* __restrict__ cnt_p, const uint32_t* __restrict__ gidx,
+                                                 uint32_t off)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        const uint32_t slot = cl[c];
+        const uint32_t s = slot / B.cap;
+        const uint32_t n = B.n[s];
+        const uint8_t* T = B.T + (size_t)s * B.cap;
+        const uint32_t v = B.sa[slot];
+        uint32_t j = (v & kIdxMask) + (off % n);
+        if (j >= n) j -= n;
+        uint64_t k = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kTextBytes; ++q) {
+            k = (k << 8) | T[j];
+            j = j + 1 == n ? 0 : j + 1;
+        }
+        B.keys_a[c] = ((uint64_t)(gidx[c] - 1) << (8 * kTextBytes)) | k;
+        B.vals_a[c] = v;
+    }
+}
+
+// refined order back into sa; still-tied flags of the list
+__global__ __launch_bounds__(256) void text_write(Batch B, const uint32_t* __restrict__ cl,
+                                                  const uint32_t* __restrict__ cnt_p)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        B.sa[cl[c]] = B.vals_b[c];
+        const uint64_t k = B.keys_b[c];
+        B.uflag[c] = ((c > 0 && B.keys_b[c - 1] == k) || (c + 1 < cnt && B.keys_b[c + 1] == k)) ? 1 : 0;
+    }
+}
+
+// fallback to doubling: rank[i] = sorted slot of rotation i for every rotation
+// (the tied ones are fixed up to their group start by text_rank_tied)
+__global__ __launch_bounds__(256) void bwt_rank_all(Batch B, size_t N)
+{
+    for (size_t slot = blockIdx.x * (size_t)blockDim.x + threadIdx.x; slot < N;
+         slot += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t s = (uint32_t)(slot / B.cap);
+        const uint32_t j = (uint32_t)(slot - (size_t)s * B.cap);
+        const uint32_t n = (B.flags[s] & kFlagHost) ? 0u : B.n[s];
+        if (j < n) B.rank[(size_t)s * B.cap + (B.sa[slot] & kIdxMask)] = j;
+    }
+}
+
+__global__ __launch_bounds__(256) void text_head_slots(const uint32_t* __restrict__ cl, const uint32_t* __restrict__ cnt_p,
+                                                       const uint32_t* __restrict__ bnd, uint32_t* __restrict__ hv)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x)
+        hv[c] = bnd[c] ? cl[c] : 0u;
+}
+
+__global__ __launch_bounds__(256) void text_rank_tied(Batch B, const uint32_t* __restrict__ cl,
+                                                      const uint32_t* __restrict__ cnt_p, const uint32_t* __restrict__ hvs)
+{
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        const uint32_t head = hvs[c];
+        const size_t o = (size_t)(head / B.cap) * B.cap;
+        B.rank[o + (B.sa[cl[c]] & kIdxMask)] = (uint32_t)(head - o);
+    }
+}
+
 // keys of a compacted doubling round: (stream slot of the group start,
 // rank[i + h]) -- groups never mix, and inside a group the order is by the
 // rank of the rotation h further on
@@ -687,14 +798,19 @@ __global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const
         pos[c] = 0xFFFFu;  // symbols not in use: never below any m
     }
     __builtin_amdgcn_wave_barrier();
+    __shared__ uint32_t front_sym[4];
     for (uint32_t c = lane; c < nin; c += 64) {
         const int32_t kc = key[wave][c];
         uint32_t r = 0;
         for (uint32_t d = 0; d < nin; ++d) r += key[wave][d] > kc ? 1u : 0u;
         pos[c] = (uint16_t)r;
+        if (r == 0) front_sym[wave] = c;
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t w0 = posw[wave][2 * lane], w1 = posw[wave][2 * lane + 1];
+    // the symbol at place 0, kept in a scalar: a repeat (m == 0, 43 % of the
+    // steps) costs one compare
+    uint32_t front = __builtin_amdgcn_readfirstlane(front_sym[wave]);
     const uint8_t* llbuf = (const uint8_t*)B.mtfv + o;
     uint8_t* mraw = B.uflag + o;
     const uint32_t j1 = min(n, j0 + kSeg);
@@ -716,6 +832,8 @@ __global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const
 #pragma unroll
             for (uint32_t q = 0; q < 4; ++q) {
                 const uint32_t c = (four >> (8 * q)) & 0xFFu;
+                if (c == front) continue;  // m = 0
+                front = c;
                 const uint32_t hi = c & 1u, ln = c >> 2;
                 const bool in_w1 = (c & 2u) != 0;
                 const uint32_t word = in_w1 ? __builtin_amdgcn_readlane(w1, ln) : __builtin_amdgcn_readlane(w0, ln);
@@ -856,59 +974,83 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
 // huffman.c BZ2_hbMakeCodeLengths, restated (nodes and heap from 1, entry 0
 // the sentinel; weights carry the depth in the low byte).
 __device__ void make_code_lengths(uint8_t* len, const uint32_t* freq, int alphaSize, int maxLen, int* heap,
-                                  int* weight, int* parent)
+                                  int* weight, int* parent, int* hw)
 {
+    // hw[k] = weight[heap[k]]: the heap compares without the second
+    // indirection (same comparisons, same order, same tree)
     for (int i = 0; i < alphaSize; ++i) weight[i + 1] = (freq[i] == 0 ? 1 : (int)freq[i]) << 8;
     while (true) {
         int nNodes = alphaSize, nHeap = 0;
         heap[0] = 0;
+        hw[0] = 0;
         weight[0] = 0;
         parent[0] = -2;
+        auto upheap = [&](int z) {
+            int zz = z;
+            const int tmp = heap[zz], tw = hw[zz];
+            while (tw < hw[zz >> 1]) {
+                heap[zz] = heap[zz >> 1];
+                hw[zz] = hw[zz >> 1];
+                zz >>= 1;
+            }
+            heap[zz] = tmp;
+            hw[zz] = tw;
+        };
+        auto downheap = [&](int z) {
+            int zz = z;
+            const int tmp = heap[zz], tw = hw[zz];
+            while (true) {
+                int yy = zz << 1;
+                if (yy > nHeap) break;
+                if (yy < nHeap && hw[yy + 1] < hw[yy]) ++yy;
+                if (tw < hw[yy]) break;
+                heap[zz] = heap[yy];
+                hw[zz] = hw[yy];
+                zz = yy;
+            }
+            heap[zz] = tmp;
+            hw[zz] = tw;
+        };
         for (int i = 1; i <= alphaSize; ++i) {
             parent[i] = -1;
             ++nHeap;
             heap[nHeap] = i;
-            int zz = nHeap, tmp = heap[zz];
-            while (weight[tmp] < weight[heap[zz >> 1]]) { heap[zz] = heap[zz >> 1]; zz >>= 1; }
-            heap[zz] = tmp;
+            hw[nHeap] = weight[i];
+            upheap(nHeap);
         }
-        auto downheap = [&](int z) {
-            int zz = z, tmp = heap[zz];
-            while (true) {
-                int yy = zz << 1;
-                if (yy > nHeap) break;
-                if (yy < nHeap && weight[heap[yy + 1]] < weight[heap[yy]]) ++yy;
-                if (weight[tmp] < weight[heap[yy]]) break;
-                heap[zz] = heap[yy];
-                zz = yy;
-            }
-            heap[zz] = tmp;
-        };
         while (nHeap > 1) {
-            const int n1 = heap[1];
+            const int n1 = heap[1], w1 = hw[1];
             heap[1] = heap[nHeap];
+            hw[1] = hw[nHeap];
             --nHeap;
             downheap(1);
-            const int n2 = heap[1];
+            const int n2 = heap[1], w2 = hw[1];
             heap[1] = heap[nHeap];
+            hw[1] = hw[nHeap];
             --nHeap;
             downheap(1);
             ++nNodes;
             parent[n1] = parent[n2] = nNodes;
-            const int w1 = weight[n1], w2 = weight[n2];
             const int d1 = w1 & 0xff, d2 = w2 & 0xff;
-            weight[nNodes] = (int)(((uint32_t)w1 & 0xffffff00u) + ((uint32_t)w2 & 0xffffff00u)) | (1 + (d1 > d2 ? d1 : d2));
+            const int wn = (int)(((uint32_t)w1 & 0xffffff00u) + ((uint32_t)w2 & 0xffffff00u)) | (1 + (d1 > d2 ? d1 : d2));
+            weight[nNodes] = wn;
             parent[nNodes] = -1;
             ++nHeap;
             heap[nHeap] = nNodes;
-            int zz = nHeap, tmp = heap[zz];
-            while (weight[tmp] < weight[heap[zz >> 1]]) { heap[zz] = heap[zz >> 1]; zz >>= 1; }
-            heap[zz] = tmp;
+            hw[nHeap] = wn;
+            upheap(nHeap);
+        }
+        // depths top-down: a parent is created after its children, so walking
+        // the nodes downwards sees every parent's depth first (parent[] is
+        // overwritten by the depth); the leaves' depths are huffman.c's
+        // per-leaf parent walks
+        for (int k = nNodes; k >= 1; --k) {
+            const int p = parent[k];
+            parent[k] = p < 0 ? 0 : parent[p] + 1;
         }
         bool tooLong = false;
         for (int i = 1; i <= alphaSize; ++i) {
-            int j = 0, k = i;
-            while (parent[k] >= 0) { k = parent[k]; ++j; }
+            const int j = parent[i];
             len[i - 1] = (uint8_t)j;
             if (j > maxLen) tooLong = true;
         }
@@ -1012,6 +1154,7 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
 __global__ __launch_bounds__(256) void huff_lengths(Batch B)
 {
     __shared__ int hb_heap[4][kMaxAlpha + 2];
+    __shared__ int hb_hw[4][kMaxAlpha + 2];
     __shared__ int hb_weight[4][kMaxAlpha * 2];
     __shared__ int hb_parent[4][kMaxAlpha * 2];
     __shared__ uint32_t fr[4][kMaxAlpha];
@@ -1024,7 +1167,9 @@ __global__ __launch_bounds__(256) void huff_lengths(Batch B)
     const uint32_t* rf = B.rfreq + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
     for (int v = lane; v < alphaSize; v += 64) fr[wave][v] = rf[v];
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) make_code_lengths(ln[wave], fr[wave], alphaSize, 17, hb_heap[wave], hb_weight[wave], hb_parent[wave]);
+    if (lane == 0)
+        make_code_lengths(ln[wave], fr[wave], alphaSize, 17, hb_heap[wave], hb_weight[wave], hb_parent[wave],
+                          hb_hw[wave]);
     __builtin_amdgcn_wave_barrier();
     uint8_t* len = B.len + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
     for (int v = lane; v < alphaSize; v += 64) len[v] = ln[wave][v];
@@ -1419,16 +1564,77 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
                                st, B, (const uint32_t*)soff, total);
         rank0_keys = B.keys_a;
     }
-    if (e == hipSuccess && hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess) e = hipErrorUnknown;
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B, rank0_keys);
+        hipLaunchKernelGGL(bwt_ties0, dim3(8192), dim3(256), 0, st, B, rank0_keys, N);
         e = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
     }
-    // doubling rounds over the still-tied rotations only (2.4 % of them after
-    // 6 bytes on light-field symbols)
     uint32_t* cl = B.cl0;
     uint32_t* cl_next = B.cl1;
-    uint32_t h = kKeyBytes;
+    uint32_t covered = kKeyBytes;
+    uint32_t* d_cnt2 = d_cnt + 1;
+    // text rounds over the tied list (group keys: u64 per entry in the rank
+    // area, group index / bounds in the mtfv area -- both free here)
+    {
+        uint64_t* gk = (uint64_t*)B.rank;
+        uint32_t* bnd = (uint32_t*)B.mtfv;
+        for (int r = 0; r < kTextRounds && e == hipSuccess; ++r) {
+            uint32_t cnt = 0;
+            if (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                e = hipErrorUnknown;
+                break;
+            }
+            if (cnt == 0 || cnt > (1u << 25) || (size_t)cnt * 4 > N) break;
+            uint32_t* gidx = bnd + cnt;
+            const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
+            if (r == 0) hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, cl, d_cnt, rank0_keys, gk);
+            hipLaunchKernelGGL(text_bounds, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gk, bnd);
+            e = rocprim::inclusive_scan(tmp, tmp_bytes, bnd, gidx, (size_t)cnt, rocprim::plus<uint32_t>(), st);
+            if (e != hipSuccess) break;
+            hipLaunchKernelGGL(text_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gidx, covered);
+            unsigned gbits = 1;
+            while ((1u << gbits) < cnt) ++gbits;
+            e = rocprim::radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.vals_b, cnt, 0,
+                                          8 * kTextBytes + gbits, st);
+            if (e != hipSuccess) break;
+            hipLaunchKernelGGL(text_write, dim3(grid), dim3(256), 0, st, B, cl, d_cnt);
+            covered += kTextBytes;
+            e = rocprim::select(tmp, tmp_bytes, B.keys_b, B.uflag, gk, d_cnt2, (size_t)cnt, st);
+            if (e == hipSuccess) e = rocprim::select(tmp, tmp_bytes, cl, B.uflag, cl_next, d_cnt, (size_t)cnt, st);
+            std::swap(cl, cl_next);
+        }
+        // ties left (long repeats): ranks of every rotation for doubling
+        uint32_t cnt = 0;
+        if (e == hipSuccess && (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                                hipStreamSynchronize(st) != hipSuccess))
+            e = hipErrorUnknown;
+        if (e == hipSuccess && cnt > 0) {
+            // group bounds of the remaining list: from the last text keys, or
+            // from the first-round keys when no text round ran
+            uint64_t* gsrc = gk;
+            const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
+            if (covered == kKeyBytes) {
+                gsrc = (uint64_t*)B.vals_b;  // cnt * 8 <= N * 4 when cnt <= N / 2: fall back to rank0 otherwise
+            }
+            if (covered == kKeyBytes && (size_t)cnt * 2 > N) {
+                hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B, rank0_keys);
+            } else {
+                if (covered == kKeyBytes)
+                    hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, cl, d_cnt, rank0_keys, gsrc);
+                uint32_t* bnd2 = (uint32_t*)B.keys_a;  // 2 * cnt u32 fit the keys area
+                uint32_t* hv = bnd2 + cnt;
+                uint32_t* hvs = (uint32_t*)B.cl1 == cl ? (uint32_t*)B.cl0 : (uint32_t*)B.cl1;
+                hipLaunchKernelGGL(text_bounds, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gsrc, bnd2);
+                hipLaunchKernelGGL(text_head_slots, dim3(grid), dim3(256), 0, st, cl, d_cnt, bnd2, hv);
+                e = rocprim::inclusive_scan(tmp, tmp_bytes, hv, hvs, (size_t)cnt, rocprim::maximum<uint32_t>(), st);
+                hipLaunchKernelGGL(bwt_rank_all, dim3(8192), dim3(256), 0, st, B, N);
+                hipLaunchKernelGGL(text_rank_tied, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, hvs);
+                cl_next = hvs == (uint32_t*)B.cl0 ? B.cl0 : B.cl1;
+            }
+        }
+    }
+    // doubling rounds over what the text rounds left (long repeats only)
+    uint32_t h = covered;
     const uint32_t max_n = B.cap;
     while (e == hipSuccess) {
         uint32_t cnt = 0;

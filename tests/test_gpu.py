@@ -260,6 +260,11 @@ def _bz2_cases():
         "few_syms": np.repeat(rng.integers(0, 5, 300, dtype=np.uint8), 7),
         "periodic": np.tile(np.array([7, 9], np.uint8), 5000),
         "periodic_runs": np.tile(np.array([1, 1, 1, 1, 1, 2], np.uint8), 3000),
+        # ties longer than the text rounds: the doubling fallback resolves them
+        "long_repeat": np.concatenate([np.tile(rng.integers(0, 256, 700, dtype=np.uint8), 12),
+                                       np.array([1], np.uint8)]),
+        "long_repeat_lowalpha": np.concatenate([np.tile(rng.integers(0, 4, 3000, dtype=np.uint8), 9),
+                                                np.array([9, 9], np.uint8)]),
     }
     runs = []
     for L in (1, 2, 3, 4, 5, 254, 255, 256, 259, 510, 511, 1000):
@@ -305,3 +310,21 @@ def test_gpu_bzip2_block_grid_and_symbols(lfmlib, oracle, gpu):
     for (i, coord, size), g in zip(blocks, got):
         raw = oracle.gather_block(sym[None, None], coord, size)
         assert g == bz2.compress(raw, 1), i
+
+
+def test_gpu_bzip2_host_fallback_streams(lfmlib, oracle, gpu):
+    """A stream whose RLE1 block reaches nblockMAX (runs of exactly four bytes
+    expand it by 5/4; libbzip2 would cut a second bzip2 block) and a periodic
+    stream are handed to the host library; the .lfm bytes stay identical."""
+    torch = gpu
+    runs4 = np.repeat(np.arange(190000 // 4, dtype=np.uint32) % 251, 4).astype(np.uint8)
+    d = torch.from_numpy(runs4.copy()).cuda()
+    got, flags = lfmlib.bzip2_device(d, [len(runs4), 1, 1, 1, 1], [len(runs4), 1, 1, 1, 1], 1, level=2)
+    assert flags == [1] and got == [None]
+    # through the encoder: the flagged streams are compressed on the host
+    img = np.stack([runs4[:95000].reshape(1, 95000), np.tile(np.array([[3, 7]], np.uint8), (1, 47500))])
+    img = img.reshape(1, 1, 2, 1, 95000)  # x = 95000, z = 2: two streams of one row each
+    enc = lfmlib.Encoder(device=0)
+    b, st = enc.encode(img, header_version=8, nnum=13, block_size=[95000, 1, 1, 1, 1])
+    enc.close()
+    assert b == oracle.encode(img, header_version=8, nnum=13, data_type=0, block_size=[95000, 1, 1, 1, 1])
