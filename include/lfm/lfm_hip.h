@@ -43,6 +43,13 @@ enum lfm_hip_status {
 int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uint16_t* d_out, int W, int H, int nframes,
                     int T, int family, int predictor, int video_bit, int z0, void* stream);
 
+/* Inverse of lfm_hip_predict (decode): symbols -> pixels for nframes frames
+ * starting at global frame z0; a temporal first frame (video, odd z0) needs
+ * the decoded frame z0-1 in d_prev.  ENOTINV for temporal frames of the
+ * angle / space families (their residual is not invertible). */
+int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H, int nframes,
+                      int T, int family, int predictor, int video_bit, int z0, void* stream);
+
 /* The seven spatial candidates of one frame (predictors 1..7, symbolized) in
  * one launch: candidate k goes to d_out7 + (k-1)*W*H. */
 int lfm_hip_predict_candidates(const uint16_t* d_frame, uint16_t* d_out7, int W, int H, int T, int family,

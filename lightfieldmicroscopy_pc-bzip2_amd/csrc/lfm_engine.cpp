@@ -293,6 +293,15 @@ int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int thr
 // --------------------------------------------------------------- encoder --
 // GPU bzip2 (default when a GPU is usable); env LFM_GPU_BZIP2=0 selects the
 // host library for every block (the same bytes, for comparison).
+bool gpu_decode_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("LFM_GPU_DECODE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool gpu_bzip2_enabled()
 {
     static const bool on = [] {
@@ -924,13 +933,44 @@ int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h
     });
     if (err.load()) return err.load();
     if (!predicted) return 0;
-    // inverse predictor (host, frames in parallel; on video stacks the odd
-    // frames need the decoded even frame before them)
     const int W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
     const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
     const size_t fs = (size_t)W * H;
     const uint16_t* s16 = symbuf.data();
     uint16_t* o16 = (uint16_t*)img;
+    // inverse predictor on the GPU (lfm_unpredict.hip) whenever one is
+    // visible; the host loop below is the reader of GPU-less machines (the
+    // reference decoder itself is host code, klb_imageIO.cpp:1748-1821)
+    if (gpu_decode_enabled() && lfm_hip_device_count() > 0 && h.Nnum <= 31) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        hipStream_t st = nullptr;
+        void *d_s = nullptr, *d_o = nullptr;
+        const size_t vb = fs * Z * 2;
+        int rc = 0;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipMalloc(&d_s, vb) != hipSuccess ||
+            hipMalloc(&d_o, vb) != hipSuccess)
+            rc = 3;
+        for (uint64_t v = 0; v < V && !rc; ++v) {
+            if (hipMemcpyAsync(d_s, s16 + v * Z * fs, vb, hipMemcpyHostToDevice, st) != hipSuccess) { rc = 3; break; }
+            const int hr = lfm_hip_unpredict((const uint16_t*)d_s, nullptr, (uint16_t*)d_o, W, H, Z, h.Nnum, family, k,
+                                             video, 0, st);
+            if (hr == LFM_HIP_ENOTINV) {
+                std::printf("ERROR: frames of this file cannot be inverted (temporal angle/space predictor)\n");
+                rc = 3;
+                break;
+            }
+            if (hr != LFM_HIP_OK || hipMemcpyAsync(o16 + v * Z * fs, d_o, vb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                rc = 3;
+        }
+        if (d_s) (void)hipFree(d_s);
+        if (d_o) (void)hipFree(d_o);
+        if (st) (void)hipStreamDestroy(st);
+        return rc;
+    }
+    // host inverse (frames in parallel; on video stacks the odd frames need
+    // the decoded even frame before them)
     for (int pass = 0; pass < (video ? 2 : 1); ++pass) {
         std::vector<uint64_t> frames;
         for (uint64_t v = 0; v < V; ++v)

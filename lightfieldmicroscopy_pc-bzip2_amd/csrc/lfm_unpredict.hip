@@ -1,0 +1,185 @@
+// lfm_unpredict.hip -- inverse predictor + unsymbolize on gfx950 (decode).
+//
+// Replaces the reference's inverse kernels / host loops (_unPredictorK_* in
+// lfm_Predictors*.cu:1470-2739 / space :1349-2049 / angle :1416-2587, driven
+// per frame from klb_imageIO.cpp:1748-1821).  Pixel (x, y) is
+// I = (uint16)(r + pred) with r the unsymbolized residual and pred the
+// forward formula of its (tile case, position case) evaluated on DECODED
+// neighbours; tiles temporal frames (odd z of a video stack) add
+// ((pred + P) >> 1) instead, P the decoded previous frame.  The angle / space
+// temporal residual ((I - pred) + P) >> 1 drops a bit and is not invertible
+// (the reference's inverse is wrong there too): error ENOTINV.
+//
+// Every neighbour is up and / or left (reach T+1), so one wave decodes a band
+// of 64 rows as a skewed wavefront: lane r owns row y0 + r and handles column
+// x = k - r at step k.  Row r - b has then advanced b columns further, so a
+// neighbour (x - a, y - b) inside the band was produced a + b <= 2T steps ago:
+// it is read from a 64-column LDS ring of that row.  Rows of earlier bands
+// come from the output in memory.  All 64 rows move in lock step (one wave),
+// so no barrier is needed; frames are independent (even frames first, then
+// odd temporal frames on their decoded predecessors).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "lfm_cases.h"
+#include "lfm_hip.h"
+
+namespace lfm {
+
+constexpr int kRing = 64;  // columns kept per band row (>= 2T + 1 for T <= 31)
+
+struct BandNb {
+    const uint16_t* ring;  // this wave's ring: [64 rows][kRing]
+    const uint16_t* out;   // decoded frame (rows of earlier bands)
+    int W, T, x, y, r;
+    template <int N>
+    __device__ __forceinline__ int at() const
+    {
+        int dx = 0, dy = 0;
+        if constexpr (N == NB_A) { dx = -1; }
+        if constexpr (N == NB_B) { dy = -1; }
+        if constexpr (N == NB_C) { dx = -1; dy = -1; }
+        if constexpr (N == NB_AP) { dx = -T; }
+        if constexpr (N == NB_BP) { dy = -T; }
+        if constexpr (N == NB_CP) { dx = -T; dy = -T; }
+        if constexpr (N == NB_AP1) { dx = -T - 1; }
+        if constexpr (N == NB_BP1) { dy = -T - 1; }
+        if constexpr (N == NB_ABP) { dx = -1; dy = -T; }
+        if constexpr (N == NB_BAP) { dx = -T; dy = -1; }
+        const int rr = r + dy;
+        if (rr >= 0) return ring[rr * kRing + ((x + dx) & (kRing - 1))];
+        return out[(size_t)(y + dy) * W + (x + dx)];
+    }
+};
+
+template <int FAM, int K, int TC, int UC, bool TEMP>
+__device__ __forceinline__ int inv_case(BandNb& g, int r, int P)
+{
+    constexpr int F = case_formula(FAM, K, TC, UC);
+    const int pr = eval_formula<F>(g);
+    if constexpr (!TEMP) return r + pr;
+    else if constexpr (F == F_Z) return r + P;
+    else return r + ((pr + P) >> 1);
+}
+
+struct UnFrames {
+    const uint16_t* sym;   // nz frames of symbols
+    const uint16_t* prev;  // decoded frame before frame 0 (temporal frame 0) or null
+    uint16_t* out;         // nz decoded frames
+    int W, H, T, nz, z0, video;
+    int first, step;       // this launch decodes local frames first, first + step, ...
+};
+
+template <int FAM, int K>
+__global__ __launch_bounds__(64) void unpredict_band(UnFrames p)
+{
+    __shared__ uint16_t ring[64 * kRing];
+    const int fz = p.first + (int)blockIdx.x * p.step;
+    if (fz >= p.nz) return;
+    const int r = threadIdx.x;
+    const size_t fs = (size_t)p.W * p.H;
+    const uint16_t* sym = p.sym + fz * fs;
+    uint16_t* out = p.out + fz * fs;
+    const bool temporal = p.video && ((p.z0 + fz) & 1);
+    const uint16_t* prev = temporal ? (fz ? p.out + (fz - 1) * fs : p.prev) : nullptr;
+    const int W = p.W, H = p.H, T = p.T;
+    for (int y0 = 0; y0 < H; y0 += 64) {
+        const int y = y0 + r;
+        const bool row_ok = y < H;
+        const int v = y % T, ty = y / T;
+        int u = 0, tx = 0;  // x % T and x / T, advanced with x
+        for (int k = 0; k < W + 63; ++k) {
+            const int x = k - r;
+            if (row_ok && x >= 0 && x < W) {
+                BandNb g{ring, out, W, T, x, y, r};
+                const int tc = tx == 0 ? (ty == 0 ? TC_00 : TC_0Y) : (ty == 0 ? TC_X0 : TC_XY);
+                const int uc = u == 0 ? (v > 0 ? UC_COL : UC_CORNER) : (v == 0 ? UC_ROW : UC_IN);
+                const int res = unsymbolize16(sym[(size_t)y * W + x]);
+                const int P = temporal ? (int)prev[(size_t)y * W + x] : 0;
+                int val = 0;
+                if (temporal) {
+                    switch (tc * 4 + uc) {
+#define LFM_INV(TC_, UC_) case TC_ * 4 + UC_: val = inv_case<FAM, K, TC_, UC_, true>(g, res, P); break;
+                    LFM_INV(0, 0) LFM_INV(0, 1) LFM_INV(0, 2) LFM_INV(0, 3)
+                    LFM_INV(1, 0) LFM_INV(1, 1) LFM_INV(1, 2) LFM_INV(1, 3)
+                    LFM_INV(2, 0) LFM_INV(2, 1) LFM_INV(2, 2) LFM_INV(2, 3)
+                    LFM_INV(3, 0) LFM_INV(3, 1) LFM_INV(3, 2) LFM_INV(3, 3)
+#undef LFM_INV
+                    }
+                } else {
+                    switch (tc * 4 + uc) {
+#define LFM_INV(TC_, UC_) case TC_ * 4 + UC_: val = inv_case<FAM, K, TC_, UC_, false>(g, res, P); break;
+                    LFM_INV(0, 0) LFM_INV(0, 1) LFM_INV(0, 2) LFM_INV(0, 3)
+                    LFM_INV(1, 0) LFM_INV(1, 1) LFM_INV(1, 2) LFM_INV(1, 3)
+                    LFM_INV(2, 0) LFM_INV(2, 1) LFM_INV(2, 2) LFM_INV(2, 3)
+                    LFM_INV(3, 0) LFM_INV(3, 1) LFM_INV(3, 2) LFM_INV(3, 3)
+#undef LFM_INV
+                    }
+                }
+                const uint16_t o = (uint16_t)val;
+                ring[r * kRing + (x & (kRing - 1))] = o;
+                out[(size_t)y * W + x] = o;
+                if (++u == T) {
+                    u = 0;
+                    ++tx;
+                }
+            }
+        }
+        // the band's rows are read back from memory by the next band
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+template <int FAM>
+static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st)
+{
+    const int grid = (p.nz - p.first + p.step - 1) / p.step;
+    if (grid <= 0) return hipSuccess;
+    switch (k) {
+#define LFM_K(K_) case K_: hipLaunchKernelGGL((unpredict_band<FAM, K_>), dim3(grid), dim3(64), 0, st, p); break;
+    LFM_K(1) LFM_K(2) LFM_K(3) LFM_K(4) LFM_K(5) LFM_K(6) LFM_K(7)
+#undef LFM_K
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+} // namespace lfm
+
+extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
+                                 int nframes, int T, int family, int predictor, int video_bit, int z0, void* stream_)
+{
+    hipStream_t st = (hipStream_t)stream_;
+    if (W <= 0 || H <= 0 || nframes <= 0 || T <= 0 || T > 31 || predictor < 0 || predictor > 7 || family < 0 ||
+        family > 2)
+        return LFM_HIP_EINVAL;
+    const size_t bytes = (size_t)W * H * nframes * sizeof(uint16_t);
+    if (predictor == 0)
+        return hipMemcpyAsync(d_out, d_sym, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? LFM_HIP_OK
+                                                                                              : LFM_HIP_ERUNTIME;
+    const int video = video_bit & 1;
+    const bool any_temporal = video && (nframes > 1 || (z0 & 1));
+    if (any_temporal && family != 0) return LFM_HIP_ENOTINV;  // ((I - pred) + P) >> 1 drops a bit
+    if (video && (z0 & 1) && !d_prev) return LFM_HIP_EINVAL;
+    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1};
+    // without video every frame is spatial: one launch; with video the
+    // spatial (even global z) frames first, then the temporal ones on their
+    // decoded predecessors
+    const int passes = video ? 2 : 1;
+    for (int pass = 0; pass < passes; ++pass) {
+        if (video) {
+            const int want = pass;  // global parity decoded by this pass
+            p.first = (z0 & 1) == want ? 0 : 1;
+            p.step = 2;
+        }
+        hipError_t e = hipErrorInvalidValue;
+        switch (family) {
+        case 0: e = lfm::launch_unpredict<0>(predictor, p, st); break;
+        case 1: e = lfm::launch_unpredict<1>(predictor, p, st); break;
+        case 2: e = lfm::launch_unpredict<2>(predictor, p, st); break;
+        }
+        if (e != hipSuccess) return LFM_HIP_ERUNTIME;
+    }
+    return LFM_HIP_OK;
+}

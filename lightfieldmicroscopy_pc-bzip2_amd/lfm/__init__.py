@@ -37,7 +37,7 @@ EXPORTS = [
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
     "lfm_merge_slabs", "lfm_free", "lfm_decode_memory",
     # lfm_hip.h
-    "lfm_hip_predict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
+    "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
     "lfm_hip_bzip2_blocks",
 ]
@@ -104,6 +104,7 @@ def lib():
     L.lfm_free.restype = None
     L.lfm_decode_memory.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_int]
     L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
+    L.lfm_hip_unpredict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_predict_candidates.argtypes = [vp, vp] + [ctypes.c_int] * 4 + [vp]
     L.lfm_hip_entropy2d.argtypes = [vp, ctypes.c_uint64, f32p, vp]
     L.lfm_hip_bzip2_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
@@ -341,6 +342,14 @@ def predict_device(d_in, d_out, W, H, nframes, T, family, predictor, video=0, z0
     rc = lib().lfm_hip_predict(p(d_in), p(d_prev), p(d_out), W, H, nframes, T, FAMILIES.get(family, family),
                                predictor, video, z0, _stream(stream))
     _check(rc, "lfm_hip_predict")
+
+
+def unpredict_device(d_sym, d_out, W, H, nframes, T, family, predictor, video=0, z0=0, d_prev=None, stream=None):
+    """Inverse predictor (decode) on device tensors: symbols -> pixels."""
+    p = lambda t: None if t is None else (t.data_ptr() if hasattr(t, "data_ptr") else int(t))  # noqa: E731
+    rc = lib().lfm_hip_unpredict(p(d_sym), p(d_prev), p(d_out), W, H, nframes, T, FAMILIES.get(family, family),
+                                 predictor, video, z0, _stream(stream))
+    _check(rc, "lfm_hip_unpredict")
 
 
 def predict_candidates_device(d_frame, d_out7, W, H, T, family, stream=None):
