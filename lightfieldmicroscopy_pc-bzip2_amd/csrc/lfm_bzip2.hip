@@ -546,7 +546,7 @@ __global__ __launch_bounds__(256) void text_bounds(Batch B, const uint32_t* __re
 // key = (group index, next kTextBytes of the rotation at offset `off`)
 __global__ __launch_bounds__(256) void text_keys(Batch B, const uint32_t* __restrict__ cl,
                                                  const uint32_t* __restrict__ cnt_p, const uint32_t* __restrict__ gidx,
-                                                 uint32_t off)
+                                                 uint32_t off, uint32_t tb)
 {
     const uint32_t cnt = *cnt_p;
     for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
@@ -560,10 +560,12 @@ __global__ __launch_bounds__(256) void text_keys(Batch B, const uint32_t* __rest
         uint64_t k = 0;
 #pragma unroll
         for (uint32_t q = 0; q < kTextBytes; ++q) {
-            k = (k << 8) | T[j];
-            j = j + 1 == n ? 0 : j + 1;
+            if (q < tb) {
+                k = (k << 8) | T[j];
+                j = j + 1 == n ? 0 : j + 1;
+            }
         }
-        B.keys_a[c] = ((uint64_t)(gidx[c] - 1) << (8 * kTextBytes)) | k;
+        B.keys_a[c] = ((uint64_t)(gidx[c] - 1) << (8 * tb)) | k;
         B.vals_a[c] = v;
     }
 }
@@ -1647,21 +1649,24 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
                 e = hipErrorUnknown;
                 break;
             }
-            if (cnt == 0 || cnt > (1u << 25) || (size_t)cnt * 4 > N) break;
+            if (cnt == 0 || (size_t)cnt * 4 > N) break;
+            unsigned gbits = 1;
+            while ((1u << gbits) < cnt) ++gbits;
+            // group index above the text bytes in one 64-bit key: fewer text
+            // bytes when the tied list is longer than 2^24
+            const uint32_t tb = std::min<uint32_t>(kTextBytes, (64 - gbits) / 8);
             uint32_t* gidx = bnd + cnt;
             const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
             if (r == 0) hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, cl, d_cnt, rank0_keys, gk);
             hipLaunchKernelGGL(text_bounds, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gk, bnd);
             e = rocprim::inclusive_scan(tmp, tmp_bytes, bnd, gidx, (size_t)cnt, rocprim::plus<uint32_t>(), st);
             if (e != hipSuccess) break;
-            hipLaunchKernelGGL(text_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gidx, covered);
-            unsigned gbits = 1;
-            while ((1u << gbits) < cnt) ++gbits;
+            hipLaunchKernelGGL(text_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gidx, covered, tb);
             e = rocprim::radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.vals_b, cnt, 0,
-                                          8 * kTextBytes + gbits, st);
+                                          8 * tb + gbits, st);
             if (e != hipSuccess) break;
             hipLaunchKernelGGL(text_write, dim3(grid), dim3(256), 0, st, B, cl, d_cnt);
-            covered += kTextBytes;
+            covered += tb;
             e = rocprim::select(tmp, tmp_bytes, B.keys_b, B.uflag, gk, d_cnt2, (size_t)cnt, st);
             if (e == hipSuccess) e = rocprim::select(tmp, tmp_bytes, cl, B.uflag, cl_next, d_cnt, (size_t)cnt, st);
             std::swap(cl, cl_next);

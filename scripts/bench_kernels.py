@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--video", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--select", type=int, default=1)
+    ap.add_argument("--unpredict", type=int, default=1)
+    ap.add_argument("--decode", type=int, default=0, help="time whole-file decode of an encoded stack")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     X, Y, Z, T = a.X, a.Y, a.Z, a.T
@@ -53,6 +55,27 @@ def main():
             ms = timeit(lambda: lfm.predict_device(d, o, X, Y, Z, T, fam, k, a.video, stream=st), a.iters, st)
             print(json.dumps({"kernel": "predict", "family": fam, "k": k, "video": a.video, "ms": round(ms, 4),
                               "GBps": round(alg / ms / 1e6, 1), "frac_8TBs": round(alg / ms / 1e6 / 8000, 4)}))
+            if a.unpredict and not (a.video and fam != "tiles"):
+                lfm.predict_device(d, o, X, Y, Z, T, fam, k, a.video, stream=st)
+                r = torch.empty_like(d)
+                ms = timeit(lambda: lfm.unpredict_device(o, r, X, Y, Z, T, fam, k, a.video, stream=st),
+                            max(3, a.iters // 4), st)
+                ok = bool(torch.equal(r, d))
+                print(json.dumps({"kernel": "unpredict", "family": fam, "k": k, "video": a.video, "ms": round(ms, 4),
+                                  "GBps": round(alg / ms / 1e6, 1), "frac_8TBs": round(alg / ms / 1e6 / 8000, 4),
+                                  "exact": ok}))
+        if a.decode:
+            import time
+            lfm.set_family(fam)
+            buf, _ = lfm.Encoder(device=0).encode(d, header_version=0, nnum=T)
+            lfm.decode(buf)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                out = lfm.decode(buf)
+            dt = (time.perf_counter() - t0) / 3
+            ok = bool((torch.from_numpy(out.reshape(Z, Y, X).view("int16")) == d.cpu()).all())
+            print(json.dumps({"kernel": "decode_file", "family": fam, "s": round(dt, 4),
+                              "Mpx_per_s": round(px / dt / 1e6, 1), "bytes": len(buf), "exact": ok}))
         if a.select:
             ms = timeit(lambda: lfm.select_device(d[0], X, Y, T, fam, stream=st), max(3, a.iters // 4), st)
             print(json.dumps({"kernel": "select", "family": fam, "ms": round(ms, 4), "frame": [X, Y]}))
