@@ -37,6 +37,7 @@
 // block) or that are periodic are flagged for the host library: the output
 // stays byte-identical in every case.
 #include <hip/hip_runtime.h>
+#include <rocprim/block/block_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
@@ -374,87 +375,229 @@ __global__ __launch_bounds__(kRleThreads) void rle1_crc(Batch B)
 // preceding it (bits 24-31): after sorting, that byte IS the BWT output
 // column, so the MTF stage reads it in sorted order without a gather.
 constexpr uint32_t kIdxMask = 0x00FFFFFFu;
-constexpr uint32_t kKeyBytes = 6;  // first-round key: 6 bytes (2.4 % of rotations tie; 8 bytes: 6 more passes for 0.01 %)
+constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 % of rotations tie on symbols)
 
-// keys: the first kKeyBytes bytes of rotation i (big endian)
-__global__ __launch_bounds__(256) void bwt_init_keys(Batch B)
+// First round: every rotation by its 8-byte prefix, in two steps.
+//  bwt_bucket      one workgroup per stream: a counting sort of the rotations
+//                  by their leading 15 bits (byte 0, top 7 bits of byte 1), the
+//                  histogram in LDS; keys = the 8-byte prefix (big endian).
+//                  The stream's slot range is cut at bucket ends into chunks
+//                  of < 2 kChunk rotations (a cut after the bucket that holds
+//                  each multiple of kChunk; a bucket larger than kChunk is a
+//                  chunk of its own).
+//  bwt_chunk_sort  one workgroup per chunk: the chunk's rotations sorted by the
+//                  whole key in LDS (buckets are ordered by the key's top bits,
+//                  so sorting a run of whole buckets sorts each bucket), and
+//                  the still-tied flags (equal keys never cross a bucket).
+// On light-field symbols a 147k-rotation stream has ~1 000 buckets of at most
+// ~2 000 rotations: each rotation is read and written once per step; the
+// previous device-wide 60-bit radix sort made 8 HBM passes.  Chunks above the
+// large sorter's capacity (one bucket of > kBigCap equal-prefix rotations) go
+// to a rocPRIM segmented sort.
+constexpr uint32_t kBucketBits = 15;
+constexpr uint32_t kBuckets = 1u << kBucketBits;
+constexpr int kBucketThreads = 1024;
+constexpr uint32_t kBktTile = 4096;
+constexpr uint32_t kChunk = 1024;
+constexpr int kCsThreads = 256, kCsItems = 8;      // chunks up to 2 048 (every multi-bucket chunk)
+constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
+constexpr uint32_t kSmallCap = kCsThreads * kCsItems, kBigCap = kBigThreads * kBigItems;
+constexpr uint32_t kMaxCuts = 1024;                // >= 3 * cap / kChunk + 2
+
+// chunk lists: [0] <= kSmallCap, [1] <= kBigCap, [2] larger (rocPRIM)
+struct ChunkLists {
+    uint32_t* b[3];
+    uint32_t* e[3];
+    uint32_t* cnt;   // 3 counters
+};
+
+// stage T[i0 - 1 .. i0 + m + 8) cyclically into tile[0 .. m + 9), m = min(n - i0, kBktTile)
+__device__ __forceinline__ uint32_t bucket_tile(const uint8_t* __restrict__ T, uint32_t n, uint32_t i0, uint8_t* tile)
 {
-    const uint32_t s = blockIdx.y;
-    if (B.done[s]) return;
-    const uint32_t n = B.n[s];
-    const uint8_t* T = B.T + (size_t)s * B.cap;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        uint64_t k = 0;
-        uint32_t j = i;
-#pragma unroll
-        for (uint32_t q = 0; q < kKeyBytes; ++q) {
-            k = (k << 8) | T[j];
-            j = j + 1 == n ? 0 : j + 1;
-        }
-        B.keys_a[(size_t)s * B.cap + i] = k;
-        B.vals_a[(size_t)s * B.cap + i] = i | ((uint32_t)T[i ? i - 1 : n - 1] << 24);
+    const uint32_t t = threadIdx.x;
+    const uint32_t m = min(n - i0, kBktTile);
+    if (4 * t < m) {  // may read up to 3 bytes past n: inside the stream's cap
+        const uint32_t w = *(const uint32_t*)(T + i0 + 4 * t);
+        tile[1 + 4 * t] = (uint8_t)w;
+        tile[2 + 4 * t] = (uint8_t)(w >> 8);
+        tile[3 + 4 * t] = (uint8_t)(w >> 16);
+        tile[4 + 4 * t] = (uint8_t)(w >> 24);
     }
-}
-
-// Global first round: every stream's rotations in one radix sort with the
-// stream index above the 6-byte prefix (one device-wide sort runs at HBM
-// speed; a segmented sort walks each 150k-element segment with one
-// workgroup).  soff = exclusive offsets of the stream lengths.
-__global__ __launch_bounds__(1024) void bwt_stream_offsets(Batch B, uint32_t* __restrict__ soff)
-{
-    __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x, ns = B.nstreams;
-    const uint32_t per = (ns + 1023) / 1024;
-    const uint32_t s0 = min(ns, t * per), s1 = min(ns, s0 + per);
-    uint32_t sum = 0;
-    for (uint32_t s = s0; s < s1; ++s) sum += (B.flags[s] & kFlagHost) ? 0u : B.n[s];
-    part[t] = sum;
     __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    if (t < 8) {
+        uint32_t j = i0 + m + t;
+        while (j >= n) j -= n;
+        tile[1 + m + t] = T[j];
+    } else if (t == 8) {
+        tile[0] = T[i0 ? i0 - 1 : n - 1];
     }
-    uint32_t acc = part[t] - sum;
-    for (uint32_t s = s0; s < s1; ++s) {
-        soff[s] = acc;
-        acc += (B.flags[s] & kFlagHost) ? 0u : B.n[s];
-    }
-    if (t == 1023) soff[ns] = part[1023];
+    __syncthreads();
+    return m;
 }
 
-__global__ __launch_bounds__(256) void bwt_init_keys_global(Batch B, const uint32_t* __restrict__ soff)
+__global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists L)
 {
-    const uint32_t s = blockIdx.y;
+    __shared__ uint32_t hist[kBuckets];  // 128 KiB
+    __shared__ uint8_t tile[kBktTile + 16];
+    __shared__ uint32_t cuts[kMaxCuts];
+    __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
+    __shared__ uint32_t ccount[3], cbase[3];
+    const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
     const uint8_t* T = B.T + (size_t)s * B.cap;
-    const uint32_t base = soff[s];
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        uint64_t k = 0;
-        uint32_t j = i;
-#pragma unroll
-        for (uint32_t q = 0; q < kKeyBytes; ++q) {
-            k = (k << 8) | T[j];
-            j = j + 1 == n ? 0 : j + 1;
+    const uint32_t o = s * B.cap;
+    for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
+    if (t < 3) ccount[t] = 0;
+    // histogram of the 15-bit bucket
+    for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
+        const uint32_t m = bucket_tile(T, n, i0, tile);
+        for (uint32_t k = t; k < m; k += kBucketThreads)
+            atomicAdd(&hist[((uint32_t)tile[1 + k] << 7) | (tile[2 + k] >> 1)], 1u);
+        __syncthreads();
+    }
+    // exclusive scan of the buckets; chunk cuts at bucket ends
+    constexpr uint32_t per = kBuckets / kBucketThreads;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < per; ++q) sum += hist[t * per + q];
+    uint32_t isum = sum;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a = __shfl_up(isum, d);
+        if ((int)lane >= d) isum += a;
+    }
+    if (lane == 63) wsum[wave] = isum;
+    __syncthreads();
+    uint32_t psum = 0;
+    for (uint32_t w = 0; w < wave; ++w) psum += wsum[w];
+    const uint32_t my0 = psum + isum - sum;
+    // cut positions of this thread's buckets (ascending): after a bucket that
+    // holds a multiple of kChunk, and around a bucket larger than kChunk
+    auto cuts_of = [&](auto&& emit) {
+        uint32_t off = my0;
+        for (uint32_t q = 0; q < per; ++q) {
+            const uint32_t c = hist[t * per + q];
+            if (c) {
+                const uint32_t e = off + c;
+                if (c > kChunk) {
+                    if (off) emit(off);
+                    emit(e);
+                } else if ((e - 1) / kChunk >= (off + kChunk - 1) / kChunk && e - 1 >= kChunk) {
+                    emit(e);
+                }
+            }
+            off += c;
         }
-        B.keys_a[base + i] = ((uint64_t)s << (8 * kKeyBytes)) | k;
-        B.vals_a[base + i] = i | ((uint32_t)T[i ? i - 1 : n - 1] << 24);
+    };
+    uint32_t ncut = 0;
+    cuts_of([&](uint32_t) { ++ncut; });
+    uint32_t icut = ncut;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a = __shfl_up(icut, d);
+        if ((int)lane >= d) icut += a;
+    }
+    if (lane == 63) wcut[wave] = icut;
+    __syncthreads();
+    uint32_t pcut = 0, tcut = 0;
+    for (uint32_t w = 0; w < kBucketThreads / 64; ++w) {
+        if (w < wave) pcut += wcut[w];
+        tcut += wcut[w];
+    }
+    {
+        uint32_t at = pcut + icut - ncut;
+        cuts_of([&](uint32_t p) {
+            if (at < kMaxCuts) cuts[at] = p;
+            ++at;
+        });
+    }
+    // bucket starts for the scatter
+    {
+        uint32_t off = my0;
+        for (uint32_t q = 0; q < per; ++q) {
+            const uint32_t c = hist[t * per + q];
+            hist[t * per + q] = off;
+            off += c;
+        }
+    }
+    __syncthreads();
+    // chunks = runs between consecutive cuts (the last ends at n)
+    const uint32_t nch = min(tcut, kMaxCuts - 1) + 1;
+    uint32_t cb = 0, ce = 0, cls = 0, slot = 0;
+    if (t < nch) {
+        cb = t ? cuts[t - 1] : 0u;
+        ce = t + 1 < nch ? cuts[t] : n;
+        const uint32_t m = ce > cb ? ce - cb : 0u;
+        cls = m <= kSmallCap ? 0u : (m <= kBigCap ? 1u : 2u);
+        if (m) slot = atomicAdd(&ccount[cls], 1u);
+        else cb = ce;
+    }
+    __syncthreads();
+    if (t < 3) cbase[t] = ccount[t] ? atomicAdd(&L.cnt[t], ccount[t]) : 0u;
+    __syncthreads();
+    if (t < nch && ce > cb) {
+        L.b[cls][cbase[cls] + slot] = o + cb;
+        L.e[cls][cbase[cls] + slot] = o + ce;
+    }
+    // scatter: key = 8-byte prefix (big endian), value = start | preceding byte << 24
+    for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
+        const uint32_t m = bucket_tile(T, n, i0, tile);
+        for (uint32_t k = t; k < m; k += kBucketThreads) {
+            const uint8_t* p = tile + 1 + k;
+            uint64_t key = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) key = (key << 8) | p[q];
+            const uint32_t pos = atomicAdd(&hist[(uint32_t)(key >> 49)], 1u);
+            B.keys_a[o + pos] = key;
+            B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
+        }
+        __syncthreads();
     }
 }
 
-// sorted global order -> per-stream slots (the stream index is the key's top)
-__global__ __launch_bounds__(256) void bwt_scatter_global(Batch B, const uint32_t* __restrict__ soff,
-                                                          uint32_t total)
+// still-tied flag of sorted position j of a chunk [cb, ce) (keys_b)
+__device__ __forceinline__ uint8_t tied_flag(const uint64_t* __restrict__ K, uint32_t cb, uint32_t ce, uint32_t j,
+                                             uint64_t k)
 {
-    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
-        const uint64_t k = B.keys_b[g];
-        const uint32_t s = (uint32_t)(k >> (8 * kKeyBytes));
-        const size_t slot = (size_t)s * B.cap + (g - soff[s]);
-        B.keys_a[slot] = k;
-        B.sa[slot] = B.vals_b[g];
+    return ((j > cb && K[j - 1] == k) || (j + 1 < ce && K[j + 1] == k)) ? 1 : 0;
+}
+
+template <int TH, int IPT>
+__global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __restrict__ cbp,
+                                                     const uint32_t* __restrict__ cep)
+{
+    using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
+    __shared__ typename Sort::storage_type storage;
+    const uint32_t cb = cbp[blockIdx.x], ce = cep[blockIdx.x], m = ce - cb, t = threadIdx.x;
+    uint64_t k[IPT];
+    uint32_t v[IPT];
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = t * IPT + q;
+        k[q] = j < m ? B.keys_a[cb + j] : ~0ull;
+        v[q] = j < m ? B.vals_a[cb + j] : 0u;
     }
+    Sort().sort(k, v, storage, m);
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = t * IPT + q;
+        if (j < m) {
+            B.keys_b[cb + j] = k[q];
+            B.sa[cb + j] = v[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = cb + t * IPT + q;
+        if (j < ce) B.uflag[j] = tied_flag(B.keys_b, cb, ce, j, k[q]);
+    }
+}
+
+// flags of the chunks sorted by rocPRIM (one workgroup per chunk)
+__global__ __launch_bounds__(256) void bwt_chunk_flags(Batch B, const uint32_t* __restrict__ cbp,
+                                                       const uint32_t* __restrict__ cep)
+{
+    const uint32_t cb = cbp[blockIdx.x], ce = cep[blockIdx.x];
+    for (uint32_t j = cb + threadIdx.x; j < ce; j += blockDim.x) B.uflag[j] = tied_flag(B.keys_b, cb, ce, j, B.keys_b[j]);
 }
 
 // After the first sort (6-byte prefixes, sa): rank[sa[j]] = first
@@ -1482,7 +1625,9 @@ size_t prim_tmp_bytes(uint32_t count, uint32_t cap)
     uint32_t* v = nullptr;
     uint8_t* f = nullptr;
     size_t tmp = 0, q = 0;
-    (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, count, v, v, 0, 64);
+    const size_t max_seg = (size_t)count * (cap / kBigCap + 1);
+    (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, (unsigned)max_seg, v, v, 0,
+                                              64 - kBucketBits);
     tmp = std::max(tmp, q);
     (void)rocprim::radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, 0, 64);
     tmp = std::max(tmp, q);
@@ -1597,42 +1742,41 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     auto ok = [&]() { return (e = hipGetLastError()) == hipSuccess; };
     hipLaunchKernelGGL(gather_blocks, dim3(64, count), dim3(256), 0, st, B);
     hipLaunchKernelGGL(rle1_crc, dim3(count), dim3(kRleThreads), 0, st, B);
-    if (std::getenv("LFM_BZ2_SORT") && std::strcmp(std::getenv("LFM_BZ2_SORT"), "segmented") == 0)
-        hipLaunchKernelGGL(bwt_init_keys, dim3(32, count), dim3(256), 0, st, B);
     if (!ok()) return LFM_HIP_ERUNTIME;
     uint32_t* d_cnt = (uint32_t*)(offs + count + 1);  // two counters after offs
-    // round 0: every rotation by its first kKeyBytes bytes
-    static const bool segmented = [] {
-        const char* v = std::getenv("LFM_BZ2_SORT");
-        return v && std::strcmp(v, "segmented") == 0;
-    }();
+    // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
     const uint64_t* rank0_keys = B.keys_b;
-    if (segmented) {  // one segment per stream
-        e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
-                                                count, B.seg_begin, B.seg_end, 0, 8 * kKeyBytes, st);
-    } else {  // all streams in one sort, stream index above the prefix
-        uint32_t* soff = B.cl1;  // free until the doubling rounds
-        hipLaunchKernelGGL(bwt_stream_offsets, dim3(1), dim3(1024), 0, st, B, soff);
-        hipLaunchKernelGGL(bwt_init_keys_global, dim3(32, count), dim3(256), 0, st, B, soff);
-        uint32_t total = 0;
-        if (hipMemcpyAsync(&total, soff + count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    {
+        ChunkLists CL;
+        const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
+        for (int c = 0; c < 3; ++c) {
+            CL.b[c] = B.cl0 + c * q;
+            CL.e[c] = B.cl1 + c * q;
+        }
+        CL.cnt = d_cnt;
+        uint32_t nch[3] = {0, 0, 0};
+        if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess || hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess)
+            return LFM_HIP_ERUNTIME;
+        hipLaunchKernelGGL(bwt_bucket, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
+        if (!ok() || hipMemcpyAsync(nch, d_cnt, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
-            e = hipErrorUnknown;
-        unsigned sbits = 1;
-        while ((1u << sbits) < count) ++sbits;
-        if (e == hipSuccess && total)
-            // (one-sweep with 10-bit digits, 6 passes instead of 8, measured 6-25 % slower)
-            e = rocprim::radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.vals_b, total, 0,
-                                          8 * kKeyBytes + sbits, st);
-        if (e == hipSuccess && total)
-            hipLaunchKernelGGL(bwt_scatter_global, dim3(std::min<uint32_t>(8192, (total + 255) / 256)), dim3(256), 0,
-                               st, B, (const uint32_t*)soff, total);
-        rank0_keys = B.keys_a;
+            return LFM_HIP_ERUNTIME;
+        if (nch[0])
+            hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), dim3(nch[0]), dim3(kCsThreads), 0, st, B,
+                               CL.b[0], CL.e[0]);
+        if (nch[1])
+            hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), dim3(nch[1]), dim3(kBigThreads), 0, st, B,
+                               CL.b[1], CL.e[1]);
+        if (nch[2]) {
+            e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
+                                                    nch[2], CL.b[2], CL.e[2], 0, 64 - kBucketBits, st);
+            if (e == hipSuccess)
+                hipLaunchKernelGGL(bwt_chunk_flags, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
+        }
+        if (!ok()) return LFM_HIP_ERUNTIME;
     }
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(bwt_ties0, dim3(8192), dim3(256), 0, st, B, rank0_keys, N);
+    if (e == hipSuccess)
         e = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
-    }
     uint32_t* cl = B.cl0;
     uint32_t* cl_next = B.cl1;
     uint32_t covered = kKeyBytes;
