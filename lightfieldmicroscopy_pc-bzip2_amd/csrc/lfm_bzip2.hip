@@ -585,10 +585,19 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
         }
     }
     __syncthreads();
+    uint32_t nt = 0;
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
         const uint32_t j = cb + t * IPT + q;
-        if (j < ce) B.uflag[j] = tied_flag(B.keys_b, cb, ce, j, k[q]);
+        if (j < ce) {
+            const uint8_t f = tied_flag(B.keys_b, cb, ce, j, k[q]);
+            B.uflag[j] = f;
+            nt += f;
+        }
+    }
+    if (__any(nt)) {
+        for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
+        if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[cb / B.cap], nt);
     }
 }
 
@@ -597,7 +606,77 @@ __global__ __launch_bounds__(256) void bwt_chunk_flags(Batch B, const uint32_t* 
                                                        const uint32_t* __restrict__ cep)
 {
     const uint32_t cb = cbp[blockIdx.x], ce = cep[blockIdx.x];
-    for (uint32_t j = cb + threadIdx.x; j < ce; j += blockDim.x) B.uflag[j] = tied_flag(B.keys_b, cb, ce, j, B.keys_b[j]);
+    uint32_t nt = 0;
+    for (uint32_t j = cb + threadIdx.x; j < ce; j += blockDim.x) {
+        const uint8_t f = tied_flag(B.keys_b, cb, ce, j, B.keys_b[j]);
+        B.uflag[j] = f;
+        nt += f;
+    }
+    for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
+    if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[cb / B.cap], nt);
+}
+
+// The tied list (slots whose 8-byte prefix is shared), in slot order: per
+// stream offsets of the tie counts (one workgroup), then each stream with
+// ties compacts its flags (B.done = ties per stream -> exclusive offsets).
+__global__ __launch_bounds__(1024) void tie_offsets(Batch B, uint32_t* __restrict__ total)
+{
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, ns = B.nstreams;
+    const uint32_t per = (ns + 1023) / 1024;
+    const uint32_t s0 = min(ns, t * per), s1 = min(ns, s0 + per);
+    uint32_t sum = 0;
+    for (uint32_t s = s0; s < s1; ++s) sum += B.done[s];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t acc = part[t] - sum;
+    for (uint32_t s = s0; s < s1; ++s) {
+        const uint32_t c = B.done[s];
+        B.done[s] = c ? acc : ~0u;
+        acc += c;
+    }
+    if (t == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(256) void tie_compact(Batch B, uint32_t* __restrict__ cl)
+{
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t carry;
+    const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t base = B.done[s];
+    if (base == ~0u) return;
+    const uint32_t n = B.n[s], o = s * B.cap;
+    if (t == 0) carry = base;
+    __syncthreads();
+    for (uint32_t j0 = 0; j0 < n; j0 += 256 * 16) {
+        const uint32_t j = j0 + 16 * t;
+        uint4 w = make_uint4(0, 0, 0, 0);
+        if (j < n) w = *(const uint4*)(B.uflag + o + j);  // uflag is zero past n (cap is a multiple of 256)
+        const uint32_t c = __popc(w.x) + __popc(w.y) + __popc(w.z) + __popc(w.w);  // flags are 0 / 1 bytes
+        uint32_t inc = c;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t a = __shfl_up(inc, d);
+            if ((int)lane >= d) inc += a;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t at = carry + inc - c;
+        for (uint32_t w2 = 0; w2 < wave; ++w2) at += wsum[w2];
+        if (c) {
+            const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+            for (int q = 0; q < 16; ++q)
+                if ((words[q >> 2] >> (8 * (q & 3))) & 1u) cl[at++] = o + j + q;
+        }
+        __syncthreads();
+        if (t == 255) carry = at;
+        __syncthreads();
+    }
 }
 
 // After the first sort (6-byte prefixes, sa): rank[sa[j]] = first
@@ -976,25 +1055,28 @@ __global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const
             uint32_t sout = 0;
 #pragma unroll
             for (uint32_t q = 0; q < 4; ++q) {
-                const uint32_t c = (four >> (8 * q)) & 0xFFu;
-                if (c == front) continue;  // m = 0
-                front = c;
-                const uint32_t hi = c & 1u, ln = c >> 2;
-                const bool in_w1 = (c & 2u) != 0;
-                const uint32_t word = in_w1 ? __builtin_amdgcn_readlane(w1, ln) : __builtin_amdgcn_readlane(w0, ln);
-                const uint32_t m = (word >> (16 * hi)) & 0xFFFFu;
-                if (m != 0) {
-                    // the word of lane ln: c -> 0, its neighbour moves back if in front of c
-                    uint32_t other = (word >> (16 * (1 - hi))) & 0xFFFFu;
+                const uint32_t c = __builtin_amdgcn_readfirstlane((four >> (8 * q)) & 0xFFu);
+                front = __builtin_amdgcn_readfirstlane(front);
+                if (c != front) {  // m = 0 otherwise: a uniform scalar branch
+                    front = c;
+                    // branch-free update: both words of lane c >> 2 are read,
+                    // both VGPRs take the increment, the word holding c is
+                    // replaced by a lane-select
+                    const uint32_t ln = c >> 2, hi = c & 1u, sel = (c >> 1) & 1u;
+                    const uint32_t a = __builtin_amdgcn_readlane(w0, ln), b = __builtin_amdgcn_readlane(w1, ln);
+                    const uint32_t word = sel ? b : a;
+                    const uint32_t m = (word >> (16 * hi)) & 0xFFFFu;
+                    uint32_t other = (word >> (16 - 16 * hi)) & 0xFFFFu;
                     other += other < m ? 1u : 0u;
-                    const uint32_t nw = hi ? other : (other << 16);
+                    const uint32_t nw = other << (16 - 16 * hi);
                     const uint32_t m2 = m | (m << 16);
                     w0 = inc_below(w0, m2);
                     w1 = inc_below(w1, m2);
-                    if (in_w1) w1 = writelane(w1, nw, ln);
-                    else w0 = writelane(w0, nw, ln);
+                    const uint32_t l0 = sel ? 64u : ln, l1 = sel ? ln : 64u;
+                    w0 = lane == l0 ? nw : w0;
+                    w1 = lane == l1 ? nw : w1;
+                    sout |= (m & 0xFFu) << (8 * q);
                 }
-                sout |= (m & 0xFFu) << (8 * q);
             }
             outw = writelane(outw, sout, g);
         }
@@ -1755,7 +1837,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         CL.cnt = d_cnt;
         uint32_t nch[3] = {0, 0, 0};
-        if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess || hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess)
+        if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess || hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess ||
+            hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         hipLaunchKernelGGL(bwt_bucket, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
         if (!ok() || hipMemcpyAsync(nch, d_cnt, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1775,8 +1858,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         if (!ok()) return LFM_HIP_ERUNTIME;
     }
-    if (e == hipSuccess)
-        e = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0), B.uflag, B.cl0, d_cnt, N, st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(tie_offsets, dim3(1), dim3(1024), 0, st, B, d_cnt);
+        hipLaunchKernelGGL(tie_compact, dim3(count), dim3(256), 0, st, B, B.cl0);
+        if (!ok()) return LFM_HIP_ERUNTIME;
+    }
     uint32_t* cl = B.cl0;
     uint32_t* cl_next = B.cl1;
     uint32_t covered = kKeyBytes;
