@@ -1276,17 +1276,25 @@ __global__ __launch_bounds__(64) void huff_init(Batch B)
     B.nsel[s] = (nMTF + kGSize - 1) / kGSize;
 }
 
+// One workgroup per stream.  The MTF symbols are staged through LDS a tile
+// of kHuffThreads selector groups at a time (coalesced 16-byte loads); each
+// thread then costs one group from LDS and adds its symbols to the chosen
+// table's frequencies.
+constexpr uint32_t kSelTileSyms = kHuffThreads * kGSize;  // 12 800 symbols (25 KiB)
+
 __global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
 {
     __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
     __shared__ uint64_t lpack[kMaxAlpha];  // the tables' lengths of a symbol, 10 bits each
+    __shared__ uint4 tbuf4[kSelTileSyms * 2 / 16];
+    const uint16_t* tbuf = (const uint16_t*)tbuf4;
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t nMTF = B.nmtf[s], nSel = B.nsel[s];
     const int nGroups = (int)B.ngroups[s];
     const int alphaSize = (int)stream_nin(B, s) + 2;
     const uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
-    const uint16_t* mtfv = B.mtfv + (size_t)s * (B.cap + 8);
+    const uint16_t* mtfv = B.mtfv + (size_t)s * (B.cap + 8);  // 16-byte aligned rows
     uint8_t* sel = B.sel + (size_t)s * B.sel_cap;
     for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rfreq[i / kMaxAlpha][i % kMaxAlpha] = 0;
     for (int v = t; v < alphaSize; v += kHuffThreads) {
@@ -1294,21 +1302,28 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
         for (int q = 0; q < nGroups; ++q) lp |= (uint64_t)len[q * kMaxAlpha + v] << (10 * q);
         lpack[v] = lp;
     }
-    __syncthreads();
-    for (uint32_t g = t; g < nSel; g += kHuffThreads) {
-        const uint32_t gs = g * kGSize, ge = min(nMTF, gs + kGSize);
-        // a group's cost under every table at once: 50 symbols x length <= 17
-        // stays below 1024 per 10-bit field (bzip2 sums UInt16 costs)
-        uint64_t acc = 0;
-        for (uint32_t i = gs; i < ge; ++i) acc += lpack[mtfv[i]];
-        int bt = -1;
-        uint32_t bc = 999999999u;
-        for (int q = 0; q < nGroups; ++q) {
-            const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
-            if (cq < bc) { bc = cq; bt = q; }
+    for (uint32_t g0 = 0; g0 < nSel; g0 += kHuffThreads) {
+        const uint32_t i0 = g0 * kGSize, i1 = min(nMTF, i0 + kSelTileSyms);
+        const uint32_t nv = (i1 - i0 + 7) / 8;  // 16-byte vectors (the row has 8 symbols of slack)
+        __syncthreads();
+        for (uint32_t v = t; v < nv; v += kHuffThreads) tbuf4[v] = *(const uint4*)(mtfv + i0 + 8 * v);
+        __syncthreads();
+        const uint32_t g = g0 + t;
+        if (g < nSel) {
+            const uint32_t gs = g * kGSize - i0, ge = min(nMTF, (g + 1) * kGSize) - i0;
+            // a group's cost under every table at once: 50 symbols x length <= 17
+            // stays below 1024 per 10-bit field (bzip2 sums UInt16 costs)
+            uint64_t acc = 0;
+            for (uint32_t i = gs; i < ge; ++i) acc += lpack[tbuf[i]];
+            int bt = -1;
+            uint32_t bc = 999999999u;
+            for (int q = 0; q < nGroups; ++q) {
+                const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
+                if (cq < bc) { bc = cq; bt = q; }
+            }
+            sel[g] = (uint8_t)bt;
+            for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][tbuf[i]], 1u);
         }
-        sel[g] = (uint8_t)bt;
-        for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][mtfv[i]], 1u);
     }
     __syncthreads();
     uint32_t* rf = B.rfreq + (size_t)s * kMaxGroups * kMaxAlpha;
@@ -1321,7 +1336,7 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
 // e * kLenTasks + l: conflict-free): heap nodes and parents as u16, heap
 // weights as u32 (124 KiB for 48 lanes).  Leaf weights are recomputed from the
 // frequencies after a too-long retry (weight = 1 + weight / 2, per retry).
-constexpr int kLenTasks = 48;
+constexpr int kLenTasks = 16;  // lanes per wave: more waves hide the heap's dependent LDS latency
 
 __global__ __launch_bounds__(64) void huff_lengths(Batch B)
 {

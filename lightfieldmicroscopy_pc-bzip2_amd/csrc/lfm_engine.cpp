@@ -141,16 +141,65 @@ int FileSink::finish(const klb_image_header& h)
     return 0;
 }
 
+PinnedBuffer::~PinnedBuffer()
+{
+    if (p_ && malloced_) std::free(p_);
+    else if (p_) (void)hipHostFree(p_);
+}
+bool PinnedBuffer::reserve(size_t n)
+{
+    if (n <= cap_) return true;
+    const size_t cap = std::max(n, cap_ + cap_ / 2);
+    void* q = nullptr;
+    if (hipHostMalloc(&q, cap, hipHostMallocDefault) != hipSuccess) {
+        // no HIP runtime (CPU-only paths): plain memory
+        (void)hipGetLastError();
+        q = std::malloc(cap);
+        if (!q) return false;
+        if (p_ && size_) std::memcpy(q, p_, size_);
+        if (p_ && malloced_) std::free(p_);
+        else if (p_) (void)hipHostFree(p_);
+        p_ = (uint8_t*)q;
+        cap_ = cap;
+        malloced_ = true;
+        return true;
+    }
+    if (p_ && size_) std::memcpy(q, p_, size_);
+    if (p_) {
+        if (malloced_) std::free(p_);
+        else (void)hipHostFree(p_);
+    }
+    p_ = (uint8_t*)q;
+    cap_ = cap;
+    malloced_ = false;
+    return true;
+}
+bool PinnedBuffer::resize(size_t n)
+{
+    if (!reserve(n)) return false;
+    size_ = n;
+    return true;
+}
+
 int MemSink::begin(const klb_image_header& h)
 {
     out_->clear();
-    out_->resize(h.getSizeInBytes(), 0);
+    if (!out_->resize(h.getSizeInBytes())) return 3;
+    std::memset(out_->data(), 0, out_->size());
     return 0;
 }
 int MemSink::append(const uint8_t* p, size_t n)
 {
-    out_->insert(out_->end(), p, p + n);
+    uint8_t* d = direct(n);
+    if (!d) return 3;
+    std::memcpy(d, p, n);
     return 0;
+}
+uint8_t* MemSink::direct(size_t n)
+{
+    const size_t at = out_->size();
+    if (!out_->resize(at + n)) return nullptr;
+    return out_->data() + at;
 }
 int MemSink::finish(const klb_image_header& h)
 {
@@ -552,7 +601,15 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         return (size_t)(v > 0 ? v : 48 * 1024) << 20;
     }();
     const size_t per_stream = lfm_hip_bzip2_workspace_bytes(1, block_bytes) + out_cap;
-    uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>((nblocks + kBzSlots - 1) / kBzSlots,
+    // batches per slot (env LFM_BZ2_BATCHES_PER_SLOT, default 1): more, smaller
+    // batches let the in-order writer's copies overlap later batches' kernels
+    static const uint64_t per_slot = [] {
+        const char* e = std::getenv("LFM_BZ2_BATCHES_PER_SLOT");
+        const long v = e ? std::atol(e) : 0;
+        return (uint64_t)(v > 0 ? v : 1);
+    }();
+    const uint64_t nway = kBzSlots * per_slot;
+    uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>((nblocks + nway - 1) / nway,
                                                                 budget / kBzSlots / per_stream));
     batch = std::min<uint64_t>(batch, ((1ull << 32) - 1) / rle_cap);
     const uint64_t nbatch = (nblocks + batch - 1) / batch;
@@ -581,6 +638,10 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     std::vector<std::vector<uint64_t>> sizes(nbatch);
     std::vector<std::vector<uint32_t>> flags(nbatch);
     std::vector<int> state(nbatch, 0);  // 0 pending, 1 ready, 2 consumed, -1 failed
+    // a sink backed by pinned memory takes each batch's payload straight from
+    // the device, in order, at its final offset (no host copy of the blocks)
+    const bool direct = sink.direct_capable();
+    std::vector<char> staged(nbatch, 1);
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<bool> abort_all{false};
@@ -600,7 +661,10 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             flags[b].assign(cnt, 0);
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
                                           ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
-            if (ok) {
+            bool any_flag = false;
+            for (uint32_t i = 0; i < cnt; ++i) any_flag |= flags[b][i] != 0;
+            staged[b] = !direct || any_flag;
+            if (ok && staged[b]) {  // through the pinned staging buffer (the writer copies block by block)
                 uint64_t tot = 0;
                 for (uint32_t i = 0; i < cnt; ++i) tot += sizes[b][i];
                 auto t0 = clk::now();
@@ -622,6 +686,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     const uint8_t* h_all = nullptr;  // host copy of the symbols, only if a stream needs the host library
     std::vector<uint8_t> in(block_bytes), out((size_t)std::ceil((float)block_bytes * 2.0f + 50.0f));
     int rc = sink.begin(h);
+    if (direct) sink.reserve_hint(h.getSizeInBytes() + nblocks * out_cap);
     uint64_t offset = 0;
     for (uint64_t b = 0; b < nbatch && !rc; ++b) {
         {
@@ -632,8 +697,23 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         if (rc) break;
         const uint64_t b0 = b * batch;
         const uint32_t cnt = (uint32_t)sizes[b].size();
+        if (!staged[b]) {
+            uint64_t tot = 0;
+            for (uint32_t i = 0; i < cnt; ++i) tot += sizes[b][i];
+            BzSlot& sl = bz_[b % nslots];
+            uint8_t* dst = sink.direct(tot);
+            auto t0 = clk::now();
+            if (!dst || hipMemcpyAsync(dst, sl.d_out, tot, hipMemcpyDeviceToHost, sl.stream) != hipSuccess ||
+                hipStreamSynchronize(sl.stream) != hipSuccess)
+                rc = 3;
+            if (st) st->d2h_ms += ms_since(t0);
+            for (uint32_t i = 0; i < cnt; ++i) {
+                offset += sizes[b][i];
+                h.blockOffset[b0 + i] = offset;
+            }
+        }
         const uint8_t* p = (const uint8_t*)bz_[b % nslots].h_out;
-        for (uint32_t i = 0; i < cnt && !rc; ++i) {
+        for (uint32_t i = 0; i < cnt && !rc && staged[b]; ++i) {
             if (flags[b][i]) {
                 if (!h_all) {
                     const size_t bytes = h.getImageSizeBytes();

@@ -39,6 +39,31 @@ public:
     virtual int begin(const klb_image_header& h) = 0;
     virtual int append(const uint8_t* p, size_t n) = 0;
     virtual int finish(const klb_image_header& h) = 0;
+    // sinks backed by pinned host memory hand out the next n bytes of the
+    // output so a device buffer can be copied straight into place
+    virtual bool direct_capable() const { return false; }
+    virtual uint8_t* direct(size_t) { return nullptr; }
+    virtual void reserve_hint(size_t) {}
+};
+
+// growable pinned host buffer (the in-memory .lfm): device-to-host copies land
+// in it at full DMA speed, and it is kept between encodes
+class PinnedBuffer {
+public:
+    PinnedBuffer() = default;
+    PinnedBuffer(const PinnedBuffer&) = delete;
+    PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+    ~PinnedBuffer();
+    bool reserve(size_t n);
+    bool resize(size_t n);
+    void clear() { size_ = 0; }
+    uint8_t* data() { return p_; }
+    const uint8_t* data() const { return p_; }
+    size_t size() const { return size_; }
+private:
+    uint8_t* p_ = nullptr;
+    size_t size_ = 0, cap_ = 0;
+    bool malloced_ = false;
 };
 class FileSink : public Sink {
 public:
@@ -52,12 +77,15 @@ private:
 };
 class MemSink : public Sink {
 public:
-    explicit MemSink(std::vector<uint8_t>* out) : out_(out) {}
+    explicit MemSink(PinnedBuffer* out) : out_(out) {}
     int begin(const klb_image_header& h) override;
     int append(const uint8_t* p, size_t n) override;
     int finish(const klb_image_header& h) override;
+    bool direct_capable() const override { return true; }
+    uint8_t* direct(size_t n) override;
+    void reserve_hint(size_t n) override { (void)out_->reserve(n); }
 private:
-    std::vector<uint8_t>* out_;
+    PinnedBuffer* out_;
 };
 
 // Compress every block of `sym` (image layout, bpp bytes per pixel) in
@@ -82,7 +110,7 @@ public:
     // img: host pointer (dev=false) or device pointer on this encoder's device
     int encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
                const SlabSpec* slab = nullptr);
-    std::vector<uint8_t> mem_out;
+    PinnedBuffer mem_out;
     int device() const { return device_; }
 
 private:
