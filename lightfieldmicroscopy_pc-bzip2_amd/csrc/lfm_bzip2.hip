@@ -1091,6 +1091,137 @@ __global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const
     }
 }
 
+// Window-parallel MTF (the default): one wave per 4096-symbol segment walks it
+// in windows of 64 positions, one lane per position, with the list state
+// (P = place of each symbol, L = symbol at each place) in LDS.  For position
+// l of a window whose symbol c occurred earlier in the window at p:
+//     m = number of distinct symbols at positions (p, l),
+// otherwise (first occurrence in the window)
+//     m = P(c) + number of distinct earlier window symbols d with P(d) > P(c),
+// P taken at the window start.  Distinct counts come from the match masks
+// (ds_or_b64 per symbol): position i is the last occurrence before l of its
+// symbol unless some k < l has i as its previous occurrence, so with
+// U_l = OR_{k<l} bit(prev_k) the distinct symbols of (p, l) are the bits of
+// lanemask_lt(l) & ~U_l above p.  After the window the list becomes the window
+// symbols by last occurrence (most recent first) followed by the old list
+// without them.
+__device__ __forceinline__ void wsync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
+
+__global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const int32_t* __restrict__ seg_last)
+{
+    __shared__ int32_t key[4][256];
+    __shared__ uint64_t mt[4][256];
+    __shared__ uint8_t Pt[4][256], Lt[4][256], inw[4][256];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t s = blockIdx.y, k = blockIdx.x * 4 + wave;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s];
+    const uint32_t js = k * kSeg;
+    if (js >= n) return;
+    const size_t o = (size_t)s * B.cap;
+    uint32_t nin = 0;
+    for (int q = 0; q < 8; ++q) nin += __popc(B.inuse[s * 8 + q]);
+    // list at js: seen symbols by last position (descending), then the unseen
+    // ones by symbol index (ascending) -- key(unseen c) = -1 - c
+    const int32_t* lb = seg_last + ((size_t)s * nseg_max + k) * 256;
+    for (uint32_t c = lane; c < 256; c += 64) {
+        const int32_t v = c < nin ? lb[c] : INT32_MIN;
+        key[wave][c] = (c < nin && v < 0) ? -1 - (int32_t)c : v;
+        inw[wave][c] = 0;
+    }
+    wsync();
+    for (uint32_t c = lane; c < nin; c += 64) {
+        const int32_t kc = key[wave][c];
+        uint32_t r = 0;
+        for (uint32_t d = 0; d < nin; ++d) r += key[wave][d] > kc ? 1u : 0u;
+        Pt[wave][c] = (uint8_t)r;
+        Lt[wave][r] = (uint8_t)c;
+    }
+    wsync();
+    const uint8_t* llbuf = (const uint8_t*)B.mtfv + o;
+    uint8_t* mraw = B.uflag + o;
+    const uint32_t je = min(n, js + kSeg);
+    const uint64_t lt = (1ull << lane) - 1ull, gt = ~lt & ~(1ull << lane);
+    for (uint32_t j0 = js; j0 < je; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool valid = j < je;
+        const uint32_t c = valid ? llbuf[j] : 0u;
+        // match mask of c in this window
+        if (valid) mt[wave][c] = 0;
+        wsync();
+        if (valid) atomicOr((unsigned long long*)&mt[wave][c], 1ull << lane);
+        wsync();
+        const uint64_t M = valid ? mt[wave][c] : 0ull;
+        const uint64_t before = M & lt;
+        const bool has_prev = before != 0ull;
+        const uint32_t p_in = has_prev ? 63u - (uint32_t)__clzll(before) : 0u;
+        const uint32_t P0 = Pt[wave][c];
+        // U = OR over lanes k < lane of bit(prev_k)  (exclusive prefix OR)
+        uint64_t U = has_prev ? (1ull << p_in) : 0ull;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t t = __shfl_up(U, d);
+            if ((int)lane >= d) U |= t;
+        }
+        U = __shfl_up(U, 1);
+        if (lane == 0) U = 0ull;
+        uint32_t m;
+        if (has_prev) {
+            m = (uint32_t)__popcll((lt & ~U) >> (p_in + 1));
+        } else {
+            m = P0;
+        }
+        // first occurrences: earlier first-occurrence symbols placed behind c
+        const uint64_t F = ballot64(valid && !has_prev);
+        for (uint64_t f = F & ~(1ull << 63); f; f &= f - 1ull) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(f);
+            const uint32_t pi = __builtin_amdgcn_readlane(P0, i);
+            m += (!has_prev && lane > i && pi > P0) ? 1u : 0u;
+        }
+        if (valid) mraw[j] = (uint8_t)m;
+        // list update: window symbols by last occurrence, then the rest
+        const bool is_last = valid && (M & gt) == 0ull;
+        const uint64_t Lw = ballot64(is_last);
+        const uint32_t nw = (uint32_t)__popcll(Lw);
+        if (is_last) inw[wave][c] = 1;
+        wsync();
+        uint32_t sym[4], fl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t p = 4 * lane + q;
+            sym[q] = Lt[wave][p];
+            fl[q] = p < nin ? inw[wave][sym[q]] : 1u;
+        }
+        uint32_t rem_before = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rem_before += (uint32_t)__popcll(ballot64(fl[q] != 0) & lt);
+        wsync();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t p = 4 * lane + q;
+            if (!fl[q]) {
+                const uint32_t np = nw + p - rem_before;
+                Lt[wave][np] = (uint8_t)sym[q];
+                Pt[wave][sym[q]] = (uint8_t)np;
+            }
+            rem_before += fl[q];
+        }
+        if (is_last) {
+            const uint32_t np = (uint32_t)__popcll(Lw & gt);
+            Lt[wave][np] = (uint8_t)c;
+            Pt[wave][c] = (uint8_t)np;
+            inw[wave][c] = 0;
+        }
+        wsync();
+    }
+}
+
 // zero-run digits of a run of z zeros (compress.c: z-1, then RUNA/RUNB by
 // bit, (z-2)/2 ... : bijective base 2)
 __device__ __forceinline__ uint32_t run_digits(uint32_t z)
@@ -1982,7 +2113,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         const dim3 g((nseg_max + 3) / 4, count);
         hipLaunchKernelGGL(mtf_last, g, dim3(256), 0, st, B, nseg_max, seg_last);
         hipLaunchKernelGGL(mtf_prefix, dim3(count), dim3(256), 0, st, B, nseg_max, seg_last);
-        hipLaunchKernelGGL(mtf_seg, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
+        static const bool seq_mtf = std::getenv("LFM_MTF") && std::strcmp(std::getenv("LFM_MTF"), "seq") == 0;
+        if (seq_mtf)
+            hipLaunchKernelGGL(mtf_seg, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
+        else
+            hipLaunchKernelGGL(mtf_win, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
         hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
     }
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
