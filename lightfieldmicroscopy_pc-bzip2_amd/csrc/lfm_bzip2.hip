@@ -161,6 +161,23 @@ __global__ __launch_bounds__(256) void gather_blocks(Batch B)
 }
 
 // ----------------------------------------------------------- RLE1 + CRC --
+// One workgroup per stream walks the raw block in tiles of kRleTile bytes,
+// kRleChunk bytes per thread (two 16-byte loads, straight from the image when
+// the block rows are 16-byte granular, else from the gathered raw block):
+//   * run summary of the chunk (first / last byte, leading / trailing run),
+//     scanned across the tile (wave shuffles, then the waves) on top of the
+//     run carried in from the previous tiles: the bzip2 run state at the
+//     chunk start (a run restarts every 255 bytes from its first byte);
+//   * the chunk's RLE1 bytes (bzlib.c ADD_CHAR_TO_BLOCK / flush_RL) counted,
+//     placed by a scan of the counts into an LDS copy of the tile's output and
+//     stored with coalesced writes;
+//   * the chunk CRC (slicing by 4, tables in LDS) from a zero register (the
+//     stream's first chunk from 0xffffffff), combined over the tile by a tree
+//     of GF(2) "shift by 32 << k zero bytes" matrices and folded into the
+//     stream CRC; the tail of the last tile is zero padding, removed at the
+//     end by the inverse shift (the CRC is linear: crc(D . 0^p) = Z^p crc(D));
+//   * inUse: bytes present (register masks, OR-reduced once) and run-length
+//     bytes (LDS atomics, rare).
 // Run summary of a byte range, combined left to right by the scan.
 struct RunSum {
     uint32_t len;    // bytes in the range (0 = identity)
@@ -169,17 +186,28 @@ struct RunSum {
     uint32_t trail;  // length of the trailing run
 };
 
+// (selects, no early returns: the scans keep RunSums in registers)
 __device__ __forceinline__ RunSum run_combine(const RunSum& a, const RunSum& b)
 {
-    if (a.len == 0) return b;
-    if (b.len == 0) return a;
+    const bool ae = a.len == 0, be = b.len == 0;
+    const bool join = a.last == b.first && !ae && !be;
     RunSum r;
     r.len = a.len + b.len;
-    r.first = a.first;
-    r.last = b.last;
-    const bool join = a.last == b.first;
-    r.lead = (a.lead == a.len && join) ? a.len + b.lead : a.lead;
-    r.trail = (b.trail == b.len && join) ? b.len + a.trail : b.trail;
+    r.first = ae ? b.first : a.first;
+    r.last = be ? a.last : b.last;
+    r.lead = ae ? b.lead : ((join && a.lead == a.len) ? a.len + b.lead : a.lead);
+    r.trail = be ? a.trail : ((join && b.trail == b.len) ? b.len + a.trail : b.trail);
+    return r;
+}
+
+__device__ __forceinline__ RunSum run_shfl_up(const RunSum& a, int d)
+{
+    RunSum r;
+    r.len = __shfl_up(a.len, d);
+    r.first = __shfl_up(a.first, d);
+    r.last = __shfl_up(a.last, d);
+    r.lead = __shfl_up(a.lead, d);
+    r.trail = __shfl_up(a.trail, d);
     return r;
 }
 
@@ -197,176 +225,240 @@ __device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f)
     }
 }
 
-// bzip2's run state machine over one chunk, started from the carried state.
-// Emission happens when a run ends (a different byte, or the 255 cap).
-template <bool WRITE>
-__device__ __forceinline__ uint32_t rle_chunk(const uint8_t* p, uint32_t len, uint32_t& ch, uint32_t& rl, uint8_t* out,
-                                              uint32_t* inuse_lds)
-{
-    uint32_t w = 0;
-    auto emit = [&](uint32_t c, uint32_t l) {
-        if (!WRITE) {
-            atomicOr(&inuse_lds[c >> 5], 1u << (c & 31));
-            if (l >= 4) atomicOr(&inuse_lds[(l - 4) >> 5], 1u << ((l - 4) & 31));
-        }
-        if (l < 4) {
-            if (WRITE)
-                for (uint32_t k = 0; k < l; ++k) out[w + k] = (uint8_t)c;
-            w += l;
-        } else {
-            if (WRITE) {
-                out[w] = (uint8_t)c; out[w + 1] = (uint8_t)c; out[w + 2] = (uint8_t)c; out[w + 3] = (uint8_t)c;
-                out[w + 4] = (uint8_t)(l - 4);
-            }
-            w += 5;
-        }
-    };
-    for_bytes(p, len, [&](uint32_t c) {
-        if (c != ch || rl == 255) {
-            if (ch < 256) emit(ch, rl);
-            ch = c;
-            rl = 1;
-        } else {
-            ++rl;
-        }
-    });
-    return w;
-}
+constexpr uint32_t kRleChunk = 32;
+constexpr uint32_t kRleTile = kRleThreads * kRleChunk;  // 16 KiB
+constexpr int kCrcLevels = 10;                          // shift by kRleChunk << k bytes, k = 0..9 (9: one tile)
+constexpr int kCrcUnshift = 14;                         // inverse shift by 2^k bytes (padding < kRleTile)
+static_assert(kRleTile == (kRleChunk << (kCrcLevels - 1)) && kRleTile == (1u << kCrcUnshift), "CRC tables");
 
-// 32x32 GF(2) matrices as 32 columns: column k = image of bit k.
+__constant__ uint32_t c_crc4[4][256];  // 4 zero feeds of a register holding byte v at byte k
+__constant__ uint32_t c_crc_shift[kCrcLevels][32];
+__constant__ uint32_t c_crc_unshift[kCrcUnshift][32];
+
+// 32x32 GF(2) matrix as 32 columns (column k = image of bit k); m is a
+// wave-uniform constant, so its columns are scalar loads
 __device__ __forceinline__ uint32_t gf2_apply(const uint32_t* m, uint32_t v)
 {
     uint32_t r = 0;
-    for (int k = 0; k < 32; ++k)
-        if ((v >> k) & 1u) r ^= m[k];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) r ^= ((v >> k) & 1u) ? m[k] : 0u;
     return r;
 }
 
-__global__ __launch_bounds__(kRleThreads) void rle1_crc(Batch B)
+template <bool FROM_IMG>
+__global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))) void rle1_crc(Batch B)
 {
-    __shared__ RunSum sums[kRleThreads];
-    __shared__ uint32_t counts[kRleThreads];
-    __shared__ uint32_t crcs[kRleThreads];
+    constexpr uint32_t NW = kRleThreads / 64;
+    __shared__ uint32_t crc4[4][256];
+    __shared__ uint8_t tout[kRleTile + kRleTile / 4 + 64];
+    __shared__ RunSum wrs[NW];
+    __shared__ uint32_t wcnt[NW], wcrc[NW];
     __shared__ uint32_t inuse[8];
-    __shared__ uint32_t mshift[32], mtmp[32], mres[32];
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
-    const uint32_t L = B.raw_len[s];
+    __shared__ RunSum s_carry;
+    __shared__ uint32_t s_wr, s_crc;
+    const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t org[5], sz[5];
+    block_box(B.g, B.first_block + s, org, sz);
+    const uint32_t rowb = sz[0] * B.g.bpp;
+    const uint32_t L = rowb * sz[1] * sz[2] * sz[3] * sz[4];
     const uint8_t* raw = B.raw + (size_t)s * B.raw_cap;
-    const uint32_t per = ((L + kRleThreads - 1) / kRleThreads + 15) & ~15u;  // 16-byte aligned chunks
-    const uint32_t c0 = min(L, t * per), c1 = min(L, c0 + per);
-    const uint32_t clen = c1 - c0;
+    auto load16 = [&](uint32_t g) -> uint4 {
+        if (FROM_IMG) {  // rows are whole 16-byte pieces at 16-byte aligned addresses
+            const uint32_t row = g / rowb, col = g - row * rowb;
+            uint32_t q = row;
+            const uint32_t y = q % sz[1]; q /= sz[1];
+            const uint32_t z = q % sz[2]; q /= sz[2];
+            const uint32_t c = q % sz[3]; q /= sz[3];
+            const size_t src = ((((size_t)(org[4] + q) * B.g.dims[3] + (org[3] + c)) * B.g.dims[2] + (org[2] + z)) *
+                                    B.g.dims[1] + (org[1] + y)) * B.g.dims[0] + org[0];
+            return *(const uint4*)(B.img + src * B.g.bpp + col);
+        } else {
+            return *(const uint4*)(raw + g);
+        }
+    };
+    for (uint32_t i = t; i < 1024; i += kRleThreads) crc4[i >> 8][i & 255] = c_crc4[i >> 8][i & 255];
     if (t < 8) inuse[t] = 0;
-    // chunk run summary + chunk CRC (from a zero register), one pass
-    RunSum rs{clen, 0, 0, 0, 0};
-    uint32_t cc = 0;
-    if (clen) {
-        bool lead_open = true;
-        uint32_t first = 256, prev = 256, lead = 0, trail = 0;
-        for_bytes(raw + c0, clen, [&](uint32_t b) {
-            if (first == 256) first = b;
-            if (lead_open) {
-                if (b == first) ++lead;
-                else lead_open = false;
-            }
-            trail = (b == prev) ? trail + 1 : 1;
-            prev = b;
-            cc = crc_feed(cc, b);
-        });
-        rs.first = first;
-        rs.last = prev;
-        rs.lead = lead;
-        rs.trail = trail;
-    }
-    sums[t] = rs;
-    crcs[t] = cc;
-    __syncthreads();
-    // exclusive scan of run summaries (Hillis-Steele on a copy; 512 entries)
-    RunSum pre{0, 0, 0, 0, 0};
-    for (uint32_t off = 1; off < kRleThreads; off <<= 1) {
-        RunSum mine = sums[t];
-        RunSum other = t >= off ? sums[t - off] : RunSum{0, 0, 0, 0, 0};
-        __syncthreads();
-        sums[t] = run_combine(other, mine);
-        __syncthreads();
-    }
-    if (t > 0) pre = sums[t - 1];
-    // carried run state: bzip2 splits a run every 255 bytes from its start
-    uint32_t ch = 256, rl = 0;
-    if (pre.len) {
-        ch = pre.last;
-        rl = (pre.trail - 1) % 255 + 1;
-    }
-    const uint32_t last_t = L ? (L - 1) / per : 0;
-    uint32_t ch2 = ch, rl2 = rl;
-    uint32_t w = rle_chunk<false>(raw + c0, clen, ch2, rl2, nullptr, inuse);
-    if (t == last_t && ch2 < 256) {  // flush_RL of the final run
-        atomicOr(&inuse[ch2 >> 5], 1u << (ch2 & 31));
-        if (rl2 >= 4) atomicOr(&inuse[(rl2 - 4) >> 5], 1u << ((rl2 - 4) & 31));
-        w += rl2 < 4 ? rl2 : 5;
-    }
-    counts[t] = w;
-    __syncthreads();
-    for (uint32_t off = 1; off < kRleThreads; off <<= 1) {
-        const uint32_t v = t >= off ? counts[t - off] : 0u;
-        __syncthreads();
-        counts[t] += v;
-        __syncthreads();
-    }
-    const uint32_t total = counts[kRleThreads - 1];
-    const uint32_t base = counts[t] - w;
-    uint8_t* T = B.T + (size_t)s * B.cap;
-    const bool host = total >= B.nblock_max || total > B.cap - 8;
-    if (!host) {
-        ch2 = ch;
-        rl2 = rl;
-        const uint32_t w2 = rle_chunk<true>(raw + c0, clen, ch2, rl2, T + base, nullptr);
-        if (t == last_t && ch2 < 256) {
-            uint8_t* o = T + base + w2;
-            if (rl2 < 4) {
-                for (uint32_t k = 0; k < rl2; ++k) o[k] = (uint8_t)ch2;
-            } else {
-                o[0] = o[1] = o[2] = o[3] = (uint8_t)ch2;
-                o[4] = (uint8_t)(rl2 - 4);
-            }
-        }
-    }
-    // CRC: crc(all) = shift_L(0xffffffff) ^ fold_t(shift_{len_t}(acc) ^ crc_t)
     if (t == 0) {
-        // one-byte zero feed, then its power `per`
-        for (int k = 0; k < 32; ++k) mshift[k] = crc_feed(1u << k, 0);
-        for (int k = 0; k < 32; ++k) mres[k] = 1u << k;
-        uint32_t e = per;
-        while (e) {
-            if (e & 1u) {
-                for (int k = 0; k < 32; ++k) mtmp[k] = gf2_apply(mshift, mres[k]);
-                for (int k = 0; k < 32; ++k) mres[k] = mtmp[k];
-            }
-            e >>= 1;
-            if (e) {
-                for (int k = 0; k < 32; ++k) mtmp[k] = gf2_apply(mshift, mshift[k]);
-                for (int k = 0; k < 32; ++k) mshift[k] = mtmp[k];
+        s_carry = RunSum{0, 0, 0, 0, 0};
+        s_wr = 0;
+        s_crc = 0;
+    }
+    uint32_t pm[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // bytes present
+    uint8_t* Tout = B.T + (size_t)s * B.cap;
+    const uint32_t wlim = B.cap - 8;  // RLE1 bytes past this are not stored (the stream goes to the host)
+    __syncthreads();
+    for (uint32_t tb = 0; tb < L; tb += kRleTile) {
+        const uint32_t g = tb + t * kRleChunk;
+        const uint32_t nv = g < L ? min(kRleChunk, L - g) : 0u;
+        uint32_t w[8];
+        {
+            uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
+            if (nv) a = load16(g);
+            if (nv > 16) b = load16(g + 16);
+            w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+            w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+        }
+        if (nv < kRleChunk) {  // zero padding past L
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                if (nv <= 4 * q) w[q] = 0;
+                else if (nv < 4 * q + 4) w[q] &= (1u << (8 * (nv - 4 * q))) - 1u;
             }
         }
-        uint32_t acc = 0xffffffffu;
-        for (uint32_t q = 0; q < kRleThreads; ++q) {
-            const uint32_t a0 = min(L, q * per), a1 = min(L, a0 + per);
-            const uint32_t ln = a1 - a0;
-            if (!ln) break;
-            if (ln == per) {
-                acc = gf2_apply(mres, acc);
+        // chunk CRC
+        uint32_t cc = g == 0 ? 0xffffffffu : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t x = cc ^ __builtin_bswap32(w[q]);
+            cc = crc4[3][x >> 24] ^ crc4[2][(x >> 16) & 255u] ^ crc4[1][(x >> 8) & 255u] ^ crc4[0][x & 255u];
+        }
+        // chunk run summary and byte presence
+        RunSum rs{nv, w[0] & 255u, 0, 0, 0};
+        {
+            uint32_t prev = 256, lead = 0, trail = 0;
+            bool lead_open = true;
+#pragma unroll
+            for (uint32_t i = 0; i < kRleChunk; ++i) {
+                if (i < nv) {
+                    const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 255u;
+                    if (lead_open) {
+                        if (c == rs.first) ++lead;
+                        else lead_open = false;
+                    }
+                    trail = c == prev ? trail + 1 : 1;
+                    prev = c;
+                    const uint32_t bit = 1u << (c & 31), wi = c >> 5;
+#pragma unroll
+                    for (uint32_t k = 0; k < 8; ++k) pm[k] |= wi == k ? bit : 0u;
+                }
+            }
+            rs.last = prev;
+            rs.lead = lead;
+            rs.trail = trail;
+        }
+        // scan of the run summaries: wave, then waves, on top of the carry
+        RunSum inc = rs;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const RunSum o = run_shfl_up(inc, d);
+            if ((int)lane >= d) inc = run_combine(o, inc);
+        }
+        RunSum exc = run_shfl_up(inc, 1);
+        if (lane == 0) exc = RunSum{0, 0, 0, 0, 0};
+        if (lane == 63) wrs[wave] = inc;
+        __syncthreads();
+        RunSum pre = s_carry;
+#pragma unroll
+        for (uint32_t w2 = 0; w2 < NW - 1; ++w2) {
+            const RunSum o = wrs[w2];
+            if (w2 < wave) pre = run_combine(pre, o);
+        }
+        pre = run_combine(pre, exc);
+        const uint32_t ch0 = pre.len ? pre.last : 256u, rl0 = pre.len ? (pre.trail - 1) % 255 + 1 : 0u;
+        const bool has_end = nv && g + nv == L;
+        // the bzip2 run state machine over the chunk; emit(c, l) for every run that ends here
+        auto walk = [&](auto&& emit) {
+            uint32_t ch = ch0, rl = rl0;
+#pragma unroll
+            for (uint32_t i = 0; i < kRleChunk; ++i) {
+                if (i < nv) {
+                    const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 255u;
+                    if (c != ch || rl == 255) {
+                        if (ch < 256) emit(ch, rl);
+                        ch = c;
+                        rl = 1;
+                    } else {
+                        ++rl;
+                    }
+                }
+            }
+            if (has_end) emit(ch, rl);  // flush_RL of the final run
+        };
+        uint32_t cnt = 0;
+        walk([&](uint32_t c, uint32_t l) {
+            if (l >= 4) {
+                atomicOr(&inuse[(l - 4) >> 5], 1u << ((l - 4) & 31));
+                cnt += 5;
             } else {
-                for (uint32_t k = 0; k < ln; ++k) acc = crc_feed(acc, 0);
+                cnt += l;
             }
-            acc ^= crcs[q];
+        });
+        uint32_t cinc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(cinc, d);
+            if ((int)lane >= d) cinc += o;
         }
-        B.crc[s] = ~acc;
+        if (lane == 63) wcnt[wave] = cinc;
+        // tile CRC: tree over the wave's chunks, then over the waves
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t o = __shfl_xor(cc, 1 << k);
+            const bool right = (lane >> k) & 1u;
+            cc = gf2_apply(c_crc_shift[k], right ? o : cc) ^ (right ? cc : o);
+        }
+        if (lane == 0) wcrc[wave] = cc;
+        __syncthreads();
+        uint32_t base = cinc - cnt, total = 0;
+        for (uint32_t w2 = 0; w2 < NW; ++w2) {
+            if (w2 < wave) base += wcnt[w2];
+            total += wcnt[w2];
+        }
+        const uint32_t wr0 = s_wr;
+        walk([&](uint32_t c, uint32_t l) {
+            const uint8_t b = (uint8_t)c;
+            if (l >= 4) {
+                tout[base] = b; tout[base + 1] = b; tout[base + 2] = b; tout[base + 3] = b;
+                tout[base + 4] = (uint8_t)(l - 4);
+                base += 5;
+            } else {
+                for (uint32_t k = 0; k < l; ++k) tout[base + k] = b;
+                base += l;
+            }
+        });
+        RunSum ncarry{0, 0, 0, 0, 0};
+        uint32_t ncrc = 0;
+        if (t == 0) {
+            ncarry = s_carry;
+            uint32_t tc = 0;
+#pragma unroll
+            for (uint32_t w2 = 0; w2 < NW; ++w2) {
+                ncarry = run_combine(ncarry, wrs[w2]);
+                tc = gf2_apply(c_crc_shift[6], tc) ^ wcrc[w2];
+            }
+            ncrc = gf2_apply(c_crc_shift[9], s_crc) ^ tc;
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < total; i += kRleThreads)
+            if (wr0 + i < wlim) Tout[wr0 + i] = tout[i];
+        if (t == 0) {
+            s_carry = ncarry;
+            s_crc = ncrc;
+            s_wr = wr0 + total;
+        }
+    }
+    // byte presence: OR over the wave, then into the LDS map
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+        uint32_t v = pm[k];
+        for (int d = 32; d > 0; d >>= 1) v |= __shfl_xor(v, d);
+        if (lane == 0 && v) atomicOr(&inuse[k], v);
+    }
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t total = s_wr;
+        uint32_t crc = s_crc;
+        const uint32_t pad = (L + kRleTile - 1) / kRleTile * kRleTile - L;
+        for (int j = 0; j < kCrcUnshift; ++j)
+            if ((pad >> j) & 1u) crc = gf2_apply(c_crc_unshift[j], crc);
+        const bool host = total >= B.nblock_max || total > wlim;
+        B.crc[s] = L ? ~crc : 0u;
         B.n[s] = total;
         B.flags[s] = host ? kFlagHost : 0u;
         B.done[s] = host ? 1u : 0u;
         B.seg_begin[s] = s * B.cap;
         B.seg_end[s] = s * B.cap + (host ? 0u : total);
     }
-    __syncthreads();
     if (t < 8) B.inuse[s * 8 + t] = inuse[t];
 }
 
@@ -1827,6 +1919,9 @@ using namespace lfm::bz;
 namespace {
 
 uint32_t host_crc_table[256];
+uint32_t host_crc4[4][256];
+uint32_t host_crc_shift[kCrcLevels][32];
+uint32_t host_crc_unshift[kCrcUnshift][32];
 bool crc_ready = false;
 
 void ensure_crc_table()
@@ -1837,6 +1932,47 @@ void ensure_crc_table()
         for (int k = 0; k < 8; ++k) c = (c & 0x80000000u) ? (c << 1) ^ 0x04c11db7u : (c << 1);
         host_crc_table[i] = c;
     }
+    // slicing-by-4 tables: 4 zero feeds of a register holding byte v at byte k
+    auto feed0 = [](uint32_t c) { return (c << 8) ^ host_crc_table[c >> 24]; };
+    for (uint32_t k = 0; k < 4; ++k)
+        for (uint32_t v = 0; v < 256; ++v) {
+            uint32_t c = v << (8 * k);
+            for (int r = 0; r < 4; ++r) c = feed0(c);
+            host_crc4[k][v] = c;
+        }
+    // one zero feed and its inverse (the table's low byte identifies its index)
+    uint32_t inv_low[256];
+    bool seen[256] = {};
+    for (uint32_t x = 0; x < 256; ++x) {
+        const uint32_t lo = host_crc_table[x] & 0xFFu;
+        if (seen[lo]) std::abort();  // never for CRC-32: the map is a bijection
+        seen[lo] = true;
+        inv_low[lo] = x;
+    }
+    auto unfeed0 = [&](uint32_t c) {
+        const uint32_t x = inv_low[c & 0xFFu];
+        return ((c ^ host_crc_table[x]) >> 8) | (x << 24);
+    };
+    auto mat_apply = [](const uint32_t* m, uint32_t v) {
+        uint32_t r = 0;
+        for (int k = 0; k < 32; ++k)
+            if ((v >> k) & 1u) r ^= m[k];
+        return r;
+    };
+    auto mat_square = [&](const uint32_t* m, uint32_t* out) {
+        for (int k = 0; k < 32; ++k) out[k] = mat_apply(m, m[k]);
+    };
+    uint32_t z[32];
+    for (int k = 0; k < 32; ++k) z[k] = feed0(1u << k);
+    for (uint32_t b = 1; b < kRleChunk; b <<= 1) {  // Z^kRleChunk
+        uint32_t t2[32];
+        mat_square(z, t2);
+        std::memcpy(z, t2, sizeof(z));
+    }
+    std::memcpy(host_crc_shift[0], z, sizeof(z));
+    for (int l = 1; l < kCrcLevels; ++l) mat_square(host_crc_shift[l - 1], host_crc_shift[l]);
+    for (int k = 0; k < 32; ++k) host_crc_unshift[0][k] = unfeed0(1u << k);
+    for (int l = 1; l < kCrcUnshift; ++l) mat_square(host_crc_unshift[l - 1], host_crc_unshift[l]);
     crc_ready = true;
 }
 
@@ -1911,7 +2047,10 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (crc_dev != dev) {
-        if (hipMemcpyToSymbol(HIP_SYMBOL(c_crc_table), host_crc_table, sizeof(host_crc_table)) != hipSuccess)
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_crc_table), host_crc_table, sizeof(host_crc_table)) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), host_crc4, sizeof(host_crc4)) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shift), host_crc_shift, sizeof(host_crc_shift)) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(c_crc_unshift), host_crc_unshift, sizeof(host_crc_unshift)) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         crc_dev = dev;
     }
@@ -1968,8 +2107,17 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
 
     hipError_t e = hipSuccess;
     auto ok = [&]() { return (e = hipGetLastError()) == hipSuccess; };
-    hipLaunchKernelGGL(gather_blocks, dim3(64, count), dim3(256), 0, st, B);
-    hipLaunchKernelGGL(rle1_crc, dim3(count), dim3(kRleThreads), 0, st, B);
+    // RLE1 reads the image directly when every block row is whole 16-byte
+    // pieces at 16-byte aligned addresses (the default uint16 96-pixel
+    // blocks); other geometries gather the blocks first
+    const bool from_img = ((uintptr_t)d_img & 15) == 0 && (bs[0] * bpp) % 16 == 0 && (dims[0] * bpp) % 16 == 0 &&
+                          ((dims[0] % bs[0]) * bpp) % 16 == 0;
+    if (from_img) {
+        hipLaunchKernelGGL(rle1_crc<true>, dim3(count), dim3(kRleThreads), 0, st, B);
+    } else {
+        hipLaunchKernelGGL(gather_blocks, dim3(64, count), dim3(256), 0, st, B);
+        hipLaunchKernelGGL(rle1_crc<false>, dim3(count), dim3(kRleThreads), 0, st, B);
+    }
     if (!ok()) return LFM_HIP_ERUNTIME;
     uint32_t* d_cnt = (uint32_t*)(offs + count + 1);  // two counters after offs
     // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)

@@ -608,12 +608,17 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         const long v = e ? std::atol(e) : 0;
         return (uint64_t)(v > 0 ? v : 1);
     }();
-    const uint64_t nway = kBzSlots * per_slot;
+    static const int slots = [] {
+        const char* e = std::getenv("LFM_BZ2_SLOTS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? std::min(v, (int)kBzSlots) : 2;
+    }();
+    const uint64_t nway = slots * per_slot;
     uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>((nblocks + nway - 1) / nway,
-                                                                budget / kBzSlots / per_stream));
+                                                                budget / slots / per_stream));
     batch = std::min<uint64_t>(batch, ((1ull << 32) - 1) / rle_cap);
     const uint64_t nbatch = (nblocks + batch - 1) / batch;
-    const int nslots = (int)std::min<uint64_t>(kBzSlots, nbatch);
+    const int nslots = (int)std::min<uint64_t>(slots, nbatch);
     const size_t ws = lfm_hip_bzip2_workspace_bytes((uint32_t)batch, block_bytes);
     for (int k = 0; k < nslots; ++k) {
         BzSlot& sl = bz_[k];

@@ -128,7 +128,7 @@ private:
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
     void* d_prev_ = nullptr; size_t d_prev_cap_ = 0;
     // GPU bzip2 pipeline slots (stream, workspace, device + pinned output)
-    static constexpr int kBzSlots = 2;
+    static constexpr int kBzSlots = 4;  // HIP streams available to the bzip2 pipeline (LFM_BZ2_SLOTS picks how many run)
     struct BzSlot {
         hipStream_t stream = nullptr;
         void* d_ws = nullptr; size_t d_ws_cap = 0;
