@@ -37,6 +37,7 @@
 // block) or that are periodic are flagged for the host library: the output
 // stays byte-identical in every case.
 #include <hip/hip_runtime.h>
+#include <rocprim/block/block_exchange.hpp>
 #include <rocprim/block/block_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -645,52 +646,96 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     }
 }
 
-// still-tied flag of sorted position j of a chunk [cb, ce) (keys_b)
-__device__ __forceinline__ uint8_t tied_flag(const uint64_t* __restrict__ K, uint32_t cb, uint32_t ce, uint32_t j,
-                                             uint64_t k)
-{
-    return ((j > cb && K[j - 1] == k) || (j + 1 < ce && K[j + 1] == k)) ? 1 : 0;
-}
-
+// The chunk's keys / values are loaded striped (element q * TH + t: coalesced),
+// sorted (rocPRIM block merge sort: thread t ends with sorted positions
+// t * IPT .. t * IPT + IPT - 1), the still-tied flags come from the
+// neighbours in registers (each thread's edge keys through LDS), and sa /
+// uflag go back striped through LDS.  The sorted keys are not stored: the few
+// consumers (tie groups) recompute them from the text (rot_key8).
 template <int TH, int IPT>
 __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __restrict__ cbp,
                                                      const uint32_t* __restrict__ cep)
 {
+    static_assert(IPT == 8, "flags are packed 8 per thread");
     using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
-    __shared__ typename Sort::storage_type storage;
+    using ExK = rocprim::block_exchange<uint64_t, TH, IPT>;
+    using ExV = rocprim::block_exchange<uint32_t, TH, IPT>;
+    constexpr uint32_t NI = TH * IPT;
+    struct Xch {
+        uint64_t first[TH], last[TH];
+        uint32_t sv[NI];
+        uint8_t fl[NI];
+    };
+    __shared__ union alignas(16) {
+        typename Sort::storage_type s;
+        typename ExK::storage_type ek;
+        typename ExV::storage_type ev;
+        Xch x;
+    } sm;
     const uint32_t cb = cbp[blockIdx.x], ce = cep[blockIdx.x], m = ce - cb, t = threadIdx.x;
     uint64_t k[IPT];
     uint32_t v[IPT];
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = t * IPT + q;
+        const uint32_t j = q * TH + t;
         k[q] = j < m ? B.keys_a[cb + j] : ~0ull;
         v[q] = j < m ? B.vals_a[cb + j] : 0u;
     }
-    Sort().sort(k, v, storage, m);
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = t * IPT + q;
-        if (j < m) {
-            B.keys_b[cb + j] = k[q];
-            B.sa[cb + j] = v[q];
-        }
-    }
+    // the sort's valid-item count refers to the blocked arrangement
+    ExK().striped_to_blocked(k, k, sm.ek);
     __syncthreads();
+    ExV().striped_to_blocked(v, v, sm.ev);
+    __syncthreads();
+    Sort().sort(k, v, sm.s, m);
+    __syncthreads();
+    sm.x.first[t] = k[0];
+    sm.x.last[t] = k[IPT - 1];
+    __syncthreads();
+    const uint64_t kprev = t ? sm.x.last[t - 1] : 0ull, knext = t + 1 < (uint32_t)TH ? sm.x.first[t + 1] : 0ull;
     uint32_t nt = 0;
+    uint64_t fpack = 0;
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = cb + t * IPT + q;
-        if (j < ce) {
-            const uint8_t f = tied_flag(B.keys_b, cb, ce, j, k[q]);
-            B.uflag[j] = f;
-            nt += f;
-        }
+        const uint32_t pos = t * IPT + q;
+        const uint64_t lo = q ? k[q - 1] : kprev, hi = q + 1 < IPT ? k[q + 1] : knext;
+        const bool f = pos < m && ((pos > 0 && lo == k[q]) || (pos + 1 < m && hi == k[q]));
+        nt += f ? 1u : 0u;
+        fpack |= (uint64_t)(f ? 1u : 0u) << (8 * q);
+    }
+    *(uint4*)&sm.x.sv[t * IPT] = make_uint4(v[0], v[1], v[2], v[3]);
+    *(uint4*)&sm.x.sv[t * IPT + 4] = make_uint4(v[4], v[5], v[6], v[7]);
+    *(uint64_t*)&sm.x.fl[t * IPT] = fpack;
+    __syncthreads();
+    for (uint32_t j = t; j < m; j += TH) {
+        B.sa[cb + j] = sm.x.sv[j];
+        B.uflag[cb + j] = sm.x.fl[j];
     }
     if (__any(nt)) {
         for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
         if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[cb / B.cap], nt);
     }
+}
+
+// the first-round key of rotation i of stream s: its 8-byte prefix, big endian
+__device__ __forceinline__ uint64_t rot_key8(const Batch& B, uint32_t s, uint32_t i)
+{
+    const uint32_t n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
+    uint64_t k = 0;
+    uint32_t j = i;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        k = (k << 8) | T[j];
+        j = j + 1 == n ? 0u : j + 1;
+    }
+    return k;
+}
+
+// still-tied flag of sorted position j of a chunk [cb, ce) (keys_b)
+__device__ __forceinline__ uint8_t tied_flag(const uint64_t* __restrict__ K, uint32_t cb, uint32_t ce, uint32_t j,
+                                             uint64_t k)
+{
+    return ((j > cb && K[j - 1] == k) || (j + 1 < ce && K[j + 1] == k)) ? 1 : 0;
 }
 
 // flags of the chunks sorted by rocPRIM (one workgroup per chunk)
@@ -775,7 +820,7 @@ __global__ __launch_bounds__(256) void tie_compact(Batch B, uint32_t* __restrict
 // sorted position of j's group, uflag[slot] = 1 where j's group has more than
 // one rotation.  Tiles of 1024 consecutive positions keep every load
 // coalesced; the group start is a running max carried across tiles.
-__global__ __launch_bounds__(1024) void bwt_rank0(Batch B, const uint64_t* __restrict__ keys)
+__global__ __launch_bounds__(1024) void bwt_rank0(Batch B)
 {
     __shared__ uint32_t wmax[16];
     __shared__ uint32_t carry;
@@ -783,17 +828,17 @@ __global__ __launch_bounds__(1024) void bwt_rank0(Batch B, const uint64_t* __res
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
     const size_t o = (size_t)s * B.cap;
-    const uint64_t* K = keys + o;
     const uint32_t* SA = B.sa + o;
+    auto K = [&](uint32_t j) { return rot_key8(B, s, SA[j] & kIdxMask); };  // keys from the text (fallback path)
     if (t == 0) carry = 0;
     __syncthreads();
     for (uint32_t j0 = 0; j0 < n; j0 += 1024) {
         const uint32_t j = j0 + t;
         bool head = false, next_head = true;
         if (j < n) {
-            const uint64_t k = K[j];
-            head = j == 0 || k != K[j - 1];
-            next_head = j + 1 >= n || K[j + 1] != k;
+            const uint64_t k = K(j);
+            head = j == 0 || k != K(j - 1);
+            next_head = j + 1 >= n || K(j + 1) != k;
         }
         uint32_t v = head ? j : 0u;
         for (int off = 1; off < 64; off <<= 1) {
@@ -824,27 +869,14 @@ __global__ __launch_bounds__(1024) void bwt_rank0(Batch B, const uint64_t* __res
 constexpr int kTextRounds = 3;
 constexpr uint32_t kTextBytes = 5;
 
-__global__ __launch_bounds__(256) void bwt_ties0(Batch B, const uint64_t* __restrict__ K, size_t N)
-{
-    for (size_t slot = blockIdx.x * (size_t)blockDim.x + threadIdx.x; slot < N;
-         slot += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t s = (uint32_t)(slot / B.cap);
-        const uint32_t j = (uint32_t)(slot - (size_t)s * B.cap);
-        const uint32_t n = (B.flags[s] & kFlagHost) ? 0u : B.n[s];
-        uint8_t f = 0;
-        if (j < n) {
-            const uint64_t k = K[slot];
-            f = ((j > 0 && K[slot - 1] == k) || (j + 1 < n && K[slot + 1] == k)) ? 1 : 0;
-        }
-        B.uflag[slot] = f;
-    }
-}
-
-__global__ __launch_bounds__(256) void text_gather_keys(const uint32_t* __restrict__ cl, const uint32_t* __restrict__ cnt_p,
-                                                        const uint64_t* __restrict__ K, uint64_t* __restrict__ gk)
+__global__ __launch_bounds__(256) void text_gather_keys(Batch B, const uint32_t* __restrict__ cl,
+                                                        const uint32_t* __restrict__ cnt_p, uint64_t* __restrict__ gk)
 {
     const uint32_t cnt = *cnt_p;
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) gk[c] = K[cl[c]];
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        const uint32_t slot = cl[c];
+        gk[c] = rot_key8(B, slot / B.cap, B.sa[slot] & kIdxMask);
+    }
 }
 
 // group starts of the tied list (equal keys, same stream)
@@ -2121,7 +2153,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (!ok()) return LFM_HIP_ERUNTIME;
     uint32_t* d_cnt = (uint32_t*)(offs + count + 1);  // two counters after offs
     // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
-    const uint64_t* rank0_keys = B.keys_b;
     {
         ChunkLists CL;
         const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
@@ -2181,7 +2212,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             const uint32_t tb = std::min<uint32_t>(kTextBytes, (64 - gbits) / 8);
             uint32_t* gidx = bnd + cnt;
             const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
-            if (r == 0) hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, cl, d_cnt, rank0_keys, gk);
+            if (r == 0) hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gk);
             hipLaunchKernelGGL(text_bounds, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gk, bnd);
             e = rocprim::inclusive_scan(tmp, tmp_bytes, bnd, gidx, (size_t)cnt, rocprim::plus<uint32_t>(), st);
             if (e != hipSuccess) break;
@@ -2209,10 +2240,10 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
                 gsrc = (uint64_t*)B.vals_b;  // cnt * 8 <= N * 4 when cnt <= N / 2: fall back to rank0 otherwise
             }
             if (covered == kKeyBytes && (size_t)cnt * 2 > N) {
-                hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B, rank0_keys);
+                hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B);
             } else {
                 if (covered == kKeyBytes)
-                    hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, cl, d_cnt, rank0_keys, gsrc);
+                    hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gsrc);
                 uint32_t* bnd2 = (uint32_t*)B.keys_a;  // 2 * cnt u32 fit the keys area
                 uint32_t* hv = bnd2 + cnt;
                 uint32_t* hvs = (uint32_t*)B.cl1 == cl ? (uint32_t*)B.cl0 : (uint32_t*)B.cl1;
