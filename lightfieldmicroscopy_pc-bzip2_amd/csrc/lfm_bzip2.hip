@@ -492,7 +492,8 @@ constexpr uint32_t kBuckets = 1u << kBucketBits;
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
 constexpr uint32_t kChunk = 1024;
-constexpr int kCsThreads = 256, kCsItems = 8;      // chunks up to 2 048 (every multi-bucket chunk)
+constexpr int kCsThreads = 512, kCsItems = 4;      // chunks up to 2 048 (every multi-bucket chunk); 512 x 4 measured
+                                                   // 10 % faster than 256 x 8
 constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
 constexpr uint32_t kSmallCap = kCsThreads * kCsItems, kBigCap = kBigThreads * kBigItems;
 constexpr uint32_t kMaxCuts = 1024;                // >= 3 * cap / kChunk + 2
@@ -656,7 +657,7 @@ template <int TH, int IPT>
 __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __restrict__ cbp,
                                                      const uint32_t* __restrict__ cep)
 {
-    static_assert(IPT == 8, "flags are packed 8 per thread");
+    static_assert(IPT == 2 || IPT == 4 || IPT == 8, "flags are packed 2, 4 or 8 per thread");
     using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
     using ExK = rocprim::block_exchange<uint64_t, TH, IPT>;
     using ExV = rocprim::block_exchange<uint32_t, TH, IPT>;
@@ -702,9 +703,15 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
         nt += f ? 1u : 0u;
         fpack |= (uint64_t)(f ? 1u : 0u) << (8 * q);
     }
-    *(uint4*)&sm.x.sv[t * IPT] = make_uint4(v[0], v[1], v[2], v[3]);
-    *(uint4*)&sm.x.sv[t * IPT + 4] = make_uint4(v[4], v[5], v[6], v[7]);
-    *(uint64_t*)&sm.x.fl[t * IPT] = fpack;
+    if constexpr (IPT == 2) {
+        *(uint2*)&sm.x.sv[t * IPT] = make_uint2(v[0], v[1]);
+        *(uint16_t*)&sm.x.fl[t * IPT] = (uint16_t)fpack;
+    } else {
+#pragma unroll
+        for (int q = 0; q < IPT; q += 4) *(uint4*)&sm.x.sv[t * IPT + q] = make_uint4(v[q], v[q + 1], v[q + 2], v[q + 3]);
+        if constexpr (IPT == 8) *(uint64_t*)&sm.x.fl[t * IPT] = fpack;
+        else *(uint32_t*)&sm.x.fl[t * IPT] = (uint32_t)fpack;
+    }
     __syncthreads();
     for (uint32_t j = t; j < m; j += TH) {
         B.sa[cb + j] = sm.x.sv[j];
@@ -1591,8 +1598,8 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
 // e * kLenTasks + l: conflict-free): heap nodes and parents as u16, heap
 // weights as u32 (124 KiB for 48 lanes).  Leaf weights are recomputed from the
 // frequencies after a too-long retry (weight = 1 + weight / 2, per retry).
-constexpr int kLenTasks = 16;  // lanes per wave: more waves hide the heap's dependent LDS latency
-
+constexpr int kLenTasks = 16;  // default lanes per wave (LFM_HUFF_LANES overrides: 1, 2, 4, 8, 16)
+template <int kLenTasks>
 __global__ __launch_bounds__(64) void huff_lengths(Batch B)
 {
     __shared__ uint16_t heap_n[(kMaxAlpha + 2) * kLenTasks];
@@ -1689,46 +1696,67 @@ __global__ __launch_bounds__(64) void huff_lengths(Batch B)
 #undef PA
 }
 
+// One wave per stream.  Selector MTF (compress.c, 6 entries): the list is a
+// register of 4-bit entries, a step finds the entry by a zero-nibble test and
+// rotates the nibbles in front of it; 64 selectors are loaded at a time and
+// walked with readlane.  Codes (BZ2_hbAssignCodes) per table in parallel:
+// code = (codes of all shorter lengths, doubled per length) + rank of the
+// symbol among the same-length symbols before it (ballots per length).
 __global__ __launch_bounds__(64) void huff_final(Batch B)
 {
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
-    const int nGroups = (int)B.ngroups[s];
+    const uint32_t nGroups = B.ngroups[s];
     const uint32_t nSel = B.nsel[s];
-    const int alphaSize = (int)stream_nin(B, s) + 2;
+    const uint32_t alphaSize = stream_nin(B, s) + 2;
     const uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
-    if (t == 0) {  // selector MTF
+    {
         const uint8_t* sel = B.sel + (size_t)s * B.sel_cap;
         uint8_t* sm = B.sel_mtf + (size_t)s * B.sel_cap;
-        uint8_t pos[kMaxGroups];
-        for (int i = 0; i < nGroups; ++i) pos[i] = (uint8_t)i;
-        for (uint32_t i = 0; i < nSel; ++i) {
-            const uint8_t ll = sel[i];
-            int j = 0;
-            uint8_t tmp = pos[j];
-            while (ll != tmp) {
-                ++j;
-                const uint8_t tmp2 = tmp;
-                tmp = pos[j];
-                pos[j] = tmp2;
+        uint32_t pos = 0x543210u;  // entry i in nibble i
+        for (uint32_t i0 = 0; i0 < nSel; i0 += 64) {
+            const uint32_t cnt = min(64u, nSel - i0);
+            const uint32_t v = lane < cnt ? sel[i0 + lane] : 0u;
+            uint32_t out = 0;
+            for (uint32_t g = 0; g < cnt; ++g) {
+                const uint32_t ll = __builtin_amdgcn_readlane(v, g);
+                const uint32_t x = pos ^ (ll * 0x111111u);
+                const uint32_t z = (x - 0x111111u) & ~x & 0x888888u;  // lowest set: the first zero nibble
+                const uint32_t j = (uint32_t)__builtin_ctz(z) >> 2;
+                const uint32_t m = (1u << (4 * (j + 1))) - 1u;
+                pos = (pos & ~m) | (((pos << 4) | ll) & m);
+                out = lane == g ? j : out;
             }
-            pos[0] = tmp;
-            sm[i] = (uint8_t)j;
+            if (lane < cnt) sm[i0 + lane] = (uint8_t)out;
         }
-    } else if (t <= (uint32_t)nGroups) {  // codes of table t - 1 (huffman.c BZ2_hbAssignCodes)
-        const int q = (int)t - 1;
+    }
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t q = 0; q < nGroups; ++q) {
         const uint8_t* lq = len + q * kMaxAlpha;
-        int minLen = 32, maxLen = 0;
-        for (int i = 0; i < alphaSize; ++i) {
-            minLen = min(minLen, (int)lq[i]);
-            maxLen = max(maxLen, (int)lq[i]);
-        }
         uint32_t* code = B.code + ((size_t)s * kMaxGroups + q) * kMaxAlpha;
-        int vec = 0;
-        for (int nl = minLen; nl <= maxLen; ++nl) {
-            for (int i = 0; i < alphaSize; ++i)
-                if (lq[i] == nl) code[i] = (uint32_t)vec++;
-            vec <<= 1;
+        uint32_t L[5], c[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t i = 64 * k + lane;
+            L[k] = i < alphaSize ? lq[i] : 0u;
+            c[k] = 0;
+        }
+        uint32_t vec = 0;
+        for (uint32_t nl = 1; nl <= 20; ++nl) {
+            uint32_t before = 0;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint64_t b = __ballot(L[k] == nl);
+                if (L[k] == nl) c[k] = vec + before + (uint32_t)__popcll(b & lt);
+                before += (uint32_t)__popcll(b);
+            }
+            // BZ2_hbAssignCodes: vec <<= 1 after every length from minLen on
+            vec = (vec + before) << 1;
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t i = 64 * k + lane;
+            if (i < alphaSize) code[i] = c[k];
         }
     }
 }
@@ -1768,9 +1796,66 @@ __device__ __forceinline__ void put_bits_hdr(uint32_t* hdr, uint32_t* words, uin
     }
 }
 
+// header items written by many threads: neighbours share words (atomicOr)
+__device__ __forceinline__ void put_bits_hdr_atomic(uint32_t* hdr, uint32_t* words, uint64_t pos, uint32_t nbits,
+                                                    uint32_t v)
+{
+    if (!nbits) return;
+    const uint32_t w = (uint32_t)(pos >> 5), o = (uint32_t)(pos & 31);
+    const uint64_t sh = ((uint64_t)v << (64 - nbits)) >> o;
+    const uint32_t hi = (uint32_t)(sh >> 32), lo = (uint32_t)sh;
+    if (w + 1 < kHdrWords) {
+        if (hi) atomicOr(&hdr[w], hi);
+        if (lo) atomicOr(&hdr[w + 1], lo);
+    } else {
+        if (hi) atomicOr(&words[w], hi);
+        if (lo) atomicOr(&words[w + 1], lo);
+    }
+}
+
+// up to 64 bits, MSB first
+__device__ __forceinline__ void put_bits64_hdr_atomic(uint32_t* hdr, uint32_t* words, uint64_t pos, uint32_t nbits,
+                                                      uint64_t v)
+{
+    if (nbits > 32) {
+        put_bits_hdr_atomic(hdr, words, pos, nbits - 32, (uint32_t)(v >> 32));
+        put_bits_hdr_atomic(hdr, words, pos + nbits - 32, 32, (uint32_t)v);
+    } else {
+        put_bits_hdr_atomic(hdr, words, pos, nbits, (uint32_t)v);
+    }
+}
+
+// exclusive scan over the workgroup (wave shuffles, then the waves); *total = sum
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total)
+{
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NT / 64; ++w) {
+        const uint32_t x = wsum[w];
+        pre += w < wave ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + inc - v;
+}
+
+// The header: the fixed fields and the mapping table by one lane, then the
+// selectors (unary MTF values) and the delta-coded code lengths as items
+// written by all threads at prefix-summed bit offsets.
 __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
 {
-    __shared__ uint32_t part[kEmitThreads];
+    __shared__ uint32_t wsum[kEmitThreads / 64];
     __shared__ uint64_t s_hdr_bits;
     __shared__ uint32_t hdr[kHdrWords];
     __shared__ uint32_t lc[kMaxGroups * kMaxAlpha];  // code | len << 24 per (table, symbol)
@@ -1823,24 +1908,66 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
                 }
         put(3, nGroups);
         put(15, nSel);
-        const uint8_t* sm = B.sel_mtf + (size_t)s * B.sel_cap;
-        for (uint32_t i = 0; i < nSel; ++i) {
-            uint32_t k = sm[i];
-            while (k >= 16) { put(16, 0xFFFFu); k -= 16; }
-            if (k) put(k, (1u << k) - 1u);
-            put(1, 0);
-        }
-        for (uint32_t q = 0; q < nGroups; ++q) {
-            const uint8_t* lq = len + q * kMaxAlpha;
-            int curr = lq[0];
-            put(5, (uint32_t)curr);
-            for (uint32_t i = 0; i < alphaSize; ++i) {
-                while (curr < lq[i]) { put(2, 2); ++curr; }
-                while (curr > lq[i]) { put(2, 3); --curr; }
-                put(1, 0);
-            }
-        }
         s_hdr_bits = p;
+    }
+    __syncthreads();
+    {
+        uint64_t p = s_hdr_bits;
+        uint32_t total = 0;
+        // selectors: MTF value k as k ones and a zero (k < nGroups <= 6)
+        {
+            const uint8_t* sm = B.sel_mtf + (size_t)s * B.sel_cap;
+            const uint32_t per = (nSel + kEmitThreads - 1) / kEmitThreads;
+            const uint32_t a = min(nSel, t * per), b = min(nSel, a + per);
+            uint32_t nb = 0;
+            for (uint32_t i = a; i < b; ++i) nb += sm[i] + 1u;
+            uint64_t q = p + block_excl_scan<kEmitThreads>(nb, wsum, &total);
+            for (uint32_t i = a; i < b; ++i) {
+                const uint32_t k = sm[i];
+                put_bits_hdr_atomic(hdr, words, q, k + 1, ((1u << k) - 1u) << 1);
+                q += k + 1;
+            }
+            p += total;
+        }
+        // code lengths: per table 5 bits of the first length, then per symbol
+        // |d| x ("10" up / "11" down) and a zero, d = change from the previous
+        {
+            const uint32_t nl = nGroups * alphaSize;
+            const uint32_t per = (nl + kEmitThreads - 1) / kEmitThreads;
+            const uint32_t a = min(nl, t * per), b = min(nl, a + per);
+            auto item = [&](uint32_t e, uint32_t& nbits, uint64_t& v) {
+                const uint32_t q = e / alphaSize, i = e - q * alphaSize;
+                const uint8_t* lq = len + q * kMaxAlpha;
+                const int cur = lq[i], prev = i ? lq[i - 1] : cur;
+                const int d = cur - prev;
+                const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+                v = 0;
+                for (uint32_t r = 0; r < ad; ++r) v = (v << 2) | (d > 0 ? 2u : 3u);
+                v <<= 1;
+                nbits = 2 * ad + 1;
+                if (i == 0) {
+                    v |= (uint64_t)cur << nbits;
+                    nbits += 5;
+                }
+            };
+            uint32_t nb = 0;
+            for (uint32_t e = a; e < b; ++e) {
+                uint32_t k;
+                uint64_t v;
+                item(e, k, v);
+                nb += k;
+            }
+            uint64_t q = p + block_excl_scan<kEmitThreads>(nb, wsum, &total);
+            for (uint32_t e = a; e < b; ++e) {
+                uint32_t k;
+                uint64_t v;
+                item(e, k, v);
+                put_bits64_hdr_atomic(hdr, words, q, k, v);
+                q += k;
+            }
+            p += total;
+        }
+        if (t == 0) s_hdr_bits = p;
     }
     __syncthreads();
     {
@@ -1871,17 +1998,11 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
     };
     uint32_t nb = 0;
     for_syms([&](uint32_t i, uint32_t v) { nb += sym_lc(i, v) >> 24; });
-    part[t] = nb;
-    __syncthreads();
-    for (uint32_t off = 1; off < kEmitThreads; off <<= 1) {
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
+    uint32_t data_bits = 0;
+    const uint32_t excl = block_excl_scan<kEmitThreads>(nb, wsum, &data_bits);
     const uint64_t data0 = s_hdr_bits;
-    const uint64_t my0 = data0 + part[t] - nb;
-    const uint64_t data_end = data0 + part[kEmitThreads - 1];
+    const uint64_t my0 = data0 + excl;
+    const uint64_t data_end = data0 + data_bits;
     if (i1 > i0) {
         // accumulate whole words locally; only the two edge words are shared
         uint64_t acc = 0;  // pending bits, left aligned at bit 63
@@ -1918,28 +2039,54 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
     }
 }
 
-// copy the streams (MSB-first words) to their byte offsets in the payload
+// copy the streams (MSB-first words) to their byte offsets in the payload:
+// one workgroup per stream; the payload words wholly inside the stream are
+// assembled from two source words (byte-swapped) and stored 4 bytes at a
+// time, the at most 3 + 3 edge bytes one by one
 __global__ __launch_bounds__(256) void compact_streams(Batch B, const uint64_t* __restrict__ offs,
                                                        uint8_t* __restrict__ payload)
 {
-    const uint32_t s = blockIdx.y;
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
     const uint32_t nbytes = B.out_bytes[s];
+    if (!nbytes) return;
     const uint32_t* words = B.words + (size_t)s * (B.out_cap / 4);
-    uint8_t* dst = payload + offs[s];
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nbytes; k += gridDim.x * blockDim.x)
-        dst[k] = (uint8_t)(words[k >> 2] >> (24 - 8 * (k & 3)));
+    const uint64_t o = offs[s], e = o + nbytes;
+    const uint64_t a0 = (o + 3) >> 2, a1 = e >> 2;
+    auto byte_at = [&](uint64_t k) { return (uint8_t)(words[k >> 2] >> (24 - 8 * (k & 3))); };
+    if (a0 >= a1) {  // no whole word: bytes only
+        for (uint64_t k = t; k < nbytes; k += 256) payload[o + k] = byte_at(k);
+        return;
+    }
+    if (t < 4 && o + t < 4 * a0) payload[o + t] = byte_at(t);
+    if (t >= 4 && t < 8 && 4 * a1 + (t - 4) < e) payload[4 * a1 + (t - 4)] = byte_at(4 * a1 + (t - 4) - o);
+    uint32_t* p32 = (uint32_t*)payload;
+    const uint32_t r = (uint32_t)((4 * a0 - o) & 3), sh = 8 * r;
+    const uint64_t j0 = (4 * a0 - o) >> 2;  // source word of the first whole payload word
+    for (uint64_t a = a0 + t; a < a1; a += 256) {
+        const uint64_t w = j0 + (a - a0);
+        const uint32_t x = r ? (words[w] << sh) | (words[w + 1] >> (32 - sh)) : words[w];
+        p32[a] = __builtin_bswap32(x);
+    }
 }
 
-__global__ void scan_offsets(const uint32_t* __restrict__ nbytes, uint32_t n, uint64_t* __restrict__ offs)
+// exclusive offsets of the streams' byte counts (one wave, 64 at a time)
+__global__ __launch_bounds__(64) void scan_offsets(const uint32_t* __restrict__ nbytes, uint32_t n,
+                                                   uint64_t* __restrict__ offs)
 {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        uint64_t acc = 0;
-        for (uint32_t i = 0; i < n; ++i) {
-            offs[i] = acc;
-            acc += nbytes[i];
+    const uint32_t lane = threadIdx.x;
+    uint64_t carry = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint64_t v = i < n ? nbytes[i] : 0u;
+        uint64_t inc = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t o = __shfl_up(inc, d);
+            if ((int)lane >= d) inc += o;
         }
-        offs[n] = acc;
+        if (i < n) offs[i] = carry + inc - v;
+        carry += __shfl(inc, 63);
     }
+    if (lane == 0) offs[n] = carry;
 }
 
 } // namespace bz
@@ -2169,9 +2316,18 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         if (!ok() || hipMemcpyAsync(nch, d_cnt, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
-        if (nch[0])
-            hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), dim3(nch[0]), dim3(kCsThreads), 0, st, B,
-                               CL.b[0], CL.e[0]);
+        static const int cs_shape = std::getenv("LFM_CS_SHAPE") ? std::atoi(std::getenv("LFM_CS_SHAPE")) : 0;
+        if (nch[0]) {
+            if (cs_shape == 1)  // 1024 threads x 2 items (same capacity)
+                hipLaunchKernelGGL((bwt_chunk_sort<2 * kCsThreads, kCsItems / 2>), dim3(nch[0]), dim3(2 * kCsThreads), 0,
+                                   st, B, CL.b[0], CL.e[0]);
+            else if (cs_shape == 2)  // 256 threads x 8 items
+                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads / 2, kCsItems * 2>), dim3(nch[0]), dim3(kCsThreads / 2), 0,
+                                   st, B, CL.b[0], CL.e[0]);
+            else
+                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), dim3(nch[0]), dim3(kCsThreads), 0, st, B,
+                                   CL.b[0], CL.e[0]);
+        }
         if (nch[1])
             hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), dim3(nch[1]), dim3(kBigThreads), 0, st, B,
                                CL.b[1], CL.e[1]);
@@ -2302,13 +2458,25 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
     for (int it = 0; it < kIters; ++it) {
         hipLaunchKernelGGL(huff_select, dim3(count), dim3(kHuffThreads), 0, st, B);
-        hipLaunchKernelGGL(huff_lengths, dim3((count * kMaxGroups + kLenTasks - 1) / kLenTasks), dim3(64), 0, st, B);
+        static const int lanes = [] {
+            const char* v = std::getenv("LFM_HUFF_LANES");
+            const int x = v ? std::atoi(v) : kLenTasks;
+            return (x == 1 || x == 2 || x == 4 || x == 8 || x == 16) ? x : kLenTasks;
+        }();
+        const dim3 g((count * kMaxGroups + lanes - 1) / lanes);
+        switch (lanes) {
+        case 1: hipLaunchKernelGGL(huff_lengths<1>, g, dim3(64), 0, st, B); break;
+        case 2: hipLaunchKernelGGL(huff_lengths<2>, g, dim3(64), 0, st, B); break;
+        case 4: hipLaunchKernelGGL(huff_lengths<4>, g, dim3(64), 0, st, B); break;
+        case 8: hipLaunchKernelGGL(huff_lengths<8>, g, dim3(64), 0, st, B); break;
+        default: hipLaunchKernelGGL(huff_lengths<16>, g, dim3(64), 0, st, B); break;
+        }
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
     if (hipMemsetAsync(B.words, 0, (size_t)count * B.out_cap, st) != hipSuccess) return LFM_HIP_ERUNTIME;
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(64), 0, st, B.out_bytes, count, offs);
-    hipLaunchKernelGGL(compact_streams, dim3(16, count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
+    hipLaunchKernelGGL(compact_streams, dim3(count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
     if (!ok()) return LFM_HIP_ERUNTIME;
     std::vector<uint32_t> nbytes(count);
     if (hipMemcpyAsync(nbytes.data(), B.out_bytes, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
