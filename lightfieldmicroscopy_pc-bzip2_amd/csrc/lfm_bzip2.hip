@@ -541,6 +541,9 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     const uint32_t n = B.n[s];
     const uint8_t* T = B.T + (size_t)s * B.cap;
     const uint32_t o = s * B.cap;
+    // the chunk sorts flag positions < n; tie_compact's 16-byte loads also
+    // see up to 15 bytes past n, which must read as "not tied"
+    if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
     for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
     if (t < 3) ccount[t] = 0;
     // histogram of the 15-bit bucket
@@ -1879,6 +1882,14 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
     }
     const uint32_t alphaSize = nin + 2;
     for (uint32_t w = t; w < kHdrWords; w += kEmitThreads) hdr[w] = 0;
+    {
+        // the word buffer is not cleared: a header that could spill past the
+        // LDS copy (OR-ed straight into memory) gets its spill words zeroed here
+        const uint64_t bound = 32 + 48 + 32 + 1 + 24 + 16 + 256 + 3 + 15 + (uint64_t)nSel * (kMaxGroups + 1) +
+                               (uint64_t)nGroups * (5 + 33ull * alphaSize);
+        if (bound >= (uint64_t)(kHdrWords - 1) * 32)
+            for (uint64_t w = kHdrWords - 1 + t; w < (bound >> 5) + 2; w += kEmitThreads) words[w] = 0;
+    }
     for (uint32_t i = t; i < nGroups * kMaxAlpha; i += kEmitThreads) lc[i] = code[i] | ((uint32_t)len[i] << 24);
     for (uint32_t i = t; i < min(nSel, kSelLds); i += kEmitThreads) sel_l[i] = sel[i];
     __syncthreads();
@@ -1970,15 +1981,6 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
         if (t == 0) s_hdr_bits = p;
     }
     __syncthreads();
-    {
-        // full header words are the header's alone; the partial last one is
-        // shared with the first symbols (atomicOr)
-        const uint64_t hb = s_hdr_bits;
-        const uint32_t full = (uint32_t)min<uint64_t>(hb >> 5, kHdrWords - 1);
-        for (uint32_t w = t; w < full; w += kEmitThreads) words[w] = hdr[w];
-        if (t == 0 && (hb >> 5) < kHdrWords - 1 && (hb & 31)) atomicOr(&words[hb >> 5], hdr[hb >> 5]);
-        if (t == 0 && (hb >> 5) >= kHdrWords - 1) atomicOr(&words[kHdrWords - 1], hdr[kHdrWords - 1]);
-    }
     // data bits: thread t codes symbols [i0, i1), read 8 at a time
     const uint32_t per = ((nMTF + kEmitThreads - 1) / kEmitThreads + 7) & ~7u;
     const uint32_t i0 = min(nMTF, t * per), i1 = min(nMTF, i0 + per);
@@ -2003,6 +2005,29 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
     const uint64_t data0 = s_hdr_bits;
     const uint64_t my0 = data0 + excl;
     const uint64_t data_end = data0 + data_bits;
+    const uint64_t hb = data0;
+    {
+        // zero the words that are OR-ed into: each thread's edge words, the end
+        // marker's; a spilled header's last word already holds header bits
+        auto zero = [&](uint64_t w) {
+            if (!(w == (hb >> 5) && (hb >> 5) >= kHdrWords - 1)) words[w] = 0;
+        };
+        if (nb) {
+            zero(my0 >> 5);
+            zero((my0 + nb - 1) >> 5);
+        }
+        if (t == 0)
+            for (uint64_t w = data_end >> 5; w <= ((data_end + 80) >> 5) + 1; ++w) zero(w);
+    }
+    __syncthreads();
+    {
+        // full header words are the header's alone; the partial last one is
+        // shared with the first symbols (atomicOr)
+        const uint32_t full = (uint32_t)min<uint64_t>(hb >> 5, kHdrWords - 1);
+        for (uint32_t w = t; w < full; w += kEmitThreads) words[w] = hdr[w];
+        if (t == 0 && (hb >> 5) < kHdrWords - 1 && (hb & 31)) atomicOr(&words[hb >> 5], hdr[hb >> 5]);
+        if (t == 0 && (hb >> 5) >= kHdrWords - 1) atomicOr(&words[kHdrWords - 1], hdr[kHdrWords - 1]);
+    }
     if (i1 > i0) {
         // accumulate whole words locally; only the two edge words are shared
         uint64_t acc = 0;  // pending bits, left aligned at bit 63
@@ -2309,7 +2334,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         CL.cnt = d_cnt;
         uint32_t nch[3] = {0, 0, 0};
-        if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess || hipMemsetAsync(B.uflag, 0, N, st) != hipSuccess ||
+        if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         hipLaunchKernelGGL(bwt_bucket, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
@@ -2473,7 +2498,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
-    if (hipMemsetAsync(B.words, 0, (size_t)count * B.out_cap, st) != hipSuccess) return LFM_HIP_ERUNTIME;
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(64), 0, st, B.out_bytes, count, offs);
     hipLaunchKernelGGL(compact_streams, dim3(count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
