@@ -1509,36 +1509,49 @@ __device__ __forceinline__ uint32_t stream_nin(const Batch& B, uint32_t s)
     return nin;
 }
 
+// compress.c's initial partition: the frequencies go to LDS (the greedy walk
+// is sequential and would otherwise wait on a global load per symbol), one
+// lane walks them, all lanes write the lengths
 __global__ __launch_bounds__(64) void huff_init(Batch B)
 {
+    __shared__ int mf[kMaxAlpha];
+    __shared__ int pgs[kMaxGroups], pge[kMaxGroups];
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t nMTF = B.nmtf[s];
     const int alphaSize = (int)stream_nin(B, s) + 2;
     const uint32_t* mfreq = B.mtf_freq + (size_t)s * kMaxAlpha;
     uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
-    if (t != 0) return;
     const int nGroups = nMTF < 200 ? 2 : nMTF < 600 ? 3 : nMTF < 1200 ? 4 : nMTF < 2400 ? 5 : 6;
-    for (int i = 0; i < kMaxGroups * kMaxAlpha; ++i) len[i] = 15;
-    int nPart = nGroups, remF = (int)nMTF, gs = 0;
-    while (nPart > 0) {
-        const int tFreq = remF / nPart;
-        int ge = gs - 1, aFreq = 0;
-        while (aFreq < tFreq && ge < alphaSize - 1) {
-            ++ge;
-            aFreq += (int)mfreq[ge];
+    for (int v = t; v < kMaxAlpha; v += 64) mf[v] = v < alphaSize ? (int)mfreq[v] : 0;
+    __syncthreads();
+    if (t == 0) {
+        int nPart = nGroups, remF = (int)nMTF, gs = 0;
+        while (nPart > 0) {
+            const int tFreq = remF / nPart;
+            int ge = gs - 1, aFreq = 0;
+            while (aFreq < tFreq && ge < alphaSize - 1) {
+                ++ge;
+                aFreq += mf[ge];
+            }
+            if (ge > gs && nPart != nGroups && nPart != 1 && ((nGroups - nPart) % 2 == 1)) {
+                aFreq -= mf[ge];
+                --ge;
+            }
+            pgs[nPart - 1] = gs;
+            pge[nPart - 1] = ge;
+            --nPart;
+            gs = ge + 1;
+            remF -= aFreq;
         }
-        if (ge > gs && nPart != nGroups && nPart != 1 && ((nGroups - nPart) % 2 == 1)) {
-            aFreq -= (int)mfreq[ge];
-            --ge;
-        }
-        for (int v = 0; v < alphaSize; ++v) len[(nPart - 1) * kMaxAlpha + v] = (v >= gs && v <= ge) ? 0 : 15;
-        --nPart;
-        gs = ge + 1;
-        remF -= aFreq;
+        B.ngroups[s] = (uint32_t)nGroups;
+        B.nsel[s] = (nMTF + kGSize - 1) / kGSize;
     }
-    B.ngroups[s] = (uint32_t)nGroups;
-    B.nsel[s] = (nMTF + kGSize - 1) / kGSize;
+    __syncthreads();
+    for (int i = t; i < kMaxGroups * kMaxAlpha; i += 64) {
+        const int q = i / kMaxAlpha, v = i - q * kMaxAlpha;
+        len[i] = (q < nGroups && v < alphaSize && v >= pgs[q] && v <= pge[q]) ? 0 : 15;
+    }
 }
 
 // One workgroup per stream.  The MTF symbols are staged through LDS a tile
