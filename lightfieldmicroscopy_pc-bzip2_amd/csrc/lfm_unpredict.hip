@@ -20,6 +20,7 @@
 // odd temporal frames on their decoded predecessors).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "lfm_cases.h"
 #include "lfm_hip.h"
 
@@ -131,11 +132,171 @@ __global__ __launch_bounds__(64) void unpredict_band(UnFrames p)
     }
 }
 
+// Same band wavefront with the latency taken out of a step: the previous
+// band's last T+1 rows stay in LDS at full width (`top`, overwritten in place
+// by this band's last T+1 rows: a column is rewritten at least 64 - 2(T+1)
+// steps after its last reader, so T <= 30), and each lane's symbols are
+// loaded 8 steps ahead (a register delay line).  No global load on the
+// dependency chain of a step; 64 + (T+1) * W * 2 B of LDS per frame.
+struct BandNb2 {
+    const uint16_t* ring;  // [64 rows][kRing]
+    const uint16_t* top;   // [T + 1 rows][W]: rows y0 - T - 1 .. y0 - 1
+    int W, TT, x, r;
+    template <int N>
+    __device__ __forceinline__ int at() const
+    {
+        int dx = 0, dy = 0;
+        if constexpr (N == NB_A) { dx = -1; }
+        if constexpr (N == NB_B) { dy = -1; }
+        if constexpr (N == NB_C) { dx = -1; dy = -1; }
+        if constexpr (N == NB_AP) { dx = -(TT - 1); }
+        if constexpr (N == NB_BP) { dy = -(TT - 1); }
+        if constexpr (N == NB_CP) { dx = -(TT - 1); dy = -(TT - 1); }
+        if constexpr (N == NB_AP1) { dx = -TT; }
+        if constexpr (N == NB_BP1) { dy = -TT; }
+        if constexpr (N == NB_ABP) { dx = -1; dy = -(TT - 1); }
+        if constexpr (N == NB_BAP) { dx = -(TT - 1); dy = -1; }
+        const int rr = r + dy;
+        if (rr >= 0) return ring[rr * kRing + ((x + dx) & (kRing - 1))];
+        return top[(TT + rr) * W + (x + dx)];
+    }
+};
+
+template <int FAM, int K, int TC, int UC, bool TEMP>
+__device__ __forceinline__ int inv_case2(BandNb2& g, int r, int P)
+{
+    constexpr int F = case_formula(FAM, K, TC, UC);
+    const int pr = eval_formula<F>(g);
+    if constexpr (!TEMP) return r + pr;
+    else if constexpr (F == F_Z) return r + P;
+    else return r + ((pr + P) >> 1);
+}
+
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ int inv_any2(BandNb2& g, int tc, int uc, int res, int P)
+{
+    switch (tc * 4 + uc) {
+#define LFM_INV(TC_, UC_) case TC_ * 4 + UC_: return inv_case2<FAM, K, TC_, UC_, TEMP>(g, res, P);
+    LFM_INV(0, 0) LFM_INV(0, 1) LFM_INV(0, 2) LFM_INV(0, 3)
+    LFM_INV(1, 0) LFM_INV(1, 1) LFM_INV(1, 2) LFM_INV(1, 3)
+    LFM_INV(2, 0) LFM_INV(2, 1) LFM_INV(2, 2) LFM_INV(2, 3)
+    LFM_INV(3, 0) LFM_INV(3, 1) LFM_INV(3, 2) LFM_INV(3, 3)
+#undef LFM_INV
+    }
+    return 0;
+}
+
+constexpr int kSymAhead = 8;
+
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ void band2(const UnFrames& p, int fz, uint16_t* ring, uint16_t* top)
+{
+    const int r = threadIdx.x;
+    const size_t fs = (size_t)p.W * p.H;
+    const uint16_t* sym = p.sym + fz * fs;
+    uint16_t* out = p.out + fz * fs;
+    const uint16_t* prev = TEMP ? (fz ? p.out + (fz - 1) * fs : p.prev) : nullptr;
+    const int W = p.W, H = p.H, T = p.T, TT = T + 1, tb = 64 - TT;
+    for (int y0 = 0; y0 < H; y0 += 64) {
+        const int y = y0 + r;
+        const bool row_ok = y < H;
+        const int v = y % T, ty = y / T;
+        const uint16_t* srow = sym + (size_t)(row_ok ? y : 0) * W;
+        const uint16_t* prow = TEMP ? prev + (size_t)(row_ok ? y : 0) * W : nullptr;
+        uint16_t* orow = out + (size_t)(row_ok ? y : 0) * W;
+        uint16_t* trow = top + (r >= tb ? r - tb : 0) * W;
+        // delay line: sq[j] holds the symbol (and previous-frame pixel) of
+        // column k - r for the step k = k0 + j of the current round
+        uint32_t sq[kSymAhead];
+#pragma unroll
+        for (int j = 0; j < kSymAhead; ++j) {
+            const int x = j - r;
+            uint32_t sv = 0;
+            if (row_ok && x >= 0 && x < W) {
+                sv = srow[x];
+                if (TEMP) sv |= (uint32_t)prow[x] << 16;
+            }
+            sq[j] = sv;
+        }
+        int u = 0, tx = 0;  // x % T and x / T, advanced with x
+        for (int k0 = 0; k0 < W + 63; k0 += kSymAhead) {
+#pragma unroll
+            for (int j = 0; j < kSymAhead; ++j) {
+                const int k = k0 + j;
+                const int x = k - r;
+                const uint32_t sv = sq[j];
+                {  // the load for step k + kSymAhead (column x + kSymAhead)
+                    const int xn = x + kSymAhead;
+                    uint32_t nv = 0;
+                    if (row_ok && xn >= 0 && xn < W) {
+                        nv = srow[xn];
+                        if (TEMP) nv |= (uint32_t)prow[xn] << 16;
+                    }
+                    sq[j] = nv;
+                }
+                if (row_ok && x >= 0 && x < W) {
+                    BandNb2 g{ring, top, W, TT, x, r};
+                    const int tc = tx == 0 ? (ty == 0 ? TC_00 : TC_0Y) : (ty == 0 ? TC_X0 : TC_XY);
+                    const int uc = u == 0 ? (v > 0 ? UC_COL : UC_CORNER) : (v == 0 ? UC_ROW : UC_IN);
+                    const int res = unsymbolize16(sv & 0xFFFFu);
+                    const int val = inv_any2<FAM, K, TEMP>(g, tc, uc, res, TEMP ? (int)(sv >> 16) : 0);
+                    const uint16_t o = (uint16_t)val;
+                    ring[r * kRing + (x & (kRing - 1))] = o;
+                    orow[x] = o;
+                    if (r >= tb) trow[x] = o;
+                    if (++u == T) {
+                        u = 0;
+                        ++tx;
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int FAM, int K>
+__global__ __launch_bounds__(64) void unpredict_band2(UnFrames p)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds2[];
+    const int fz = p.first + (int)blockIdx.x * p.step;
+    if (fz >= p.nz) return;
+    uint16_t* ring = lds2;
+    uint16_t* top = lds2 + 64 * kRing;
+    if (p.video && ((p.z0 + fz) & 1)) band2<FAM, K, true>(p, fz, ring, top);
+    else band2<FAM, K, false>(p, fz, ring, top);
+}
+
+static size_t band2_lds(const UnFrames& p) { return (size_t)(64 * kRing + (p.T + 1) * p.W) * sizeof(uint16_t); }
+
+static bool band2_ok(const UnFrames& p)
+{
+    return p.T <= 30 && band2_lds(p) <= 160 * 1024 && !std::getenv("LFM_UNPREDICT_V1");
+}
+
+template <int FAM, int K_>
+static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
+{
+    const size_t lds = band2_lds(p);
+    const void* fn = (const void*)unpredict_band2<FAM, K_>;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL((unpredict_band2<FAM, K_>), dim3(grid), dim3(64), lds, st, p);
+    return hipGetLastError();
+}
+
 template <int FAM>
 static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st)
 {
     const int grid = (p.nz - p.first + p.step - 1) / p.step;
     if (grid <= 0) return hipSuccess;
+    if (band2_ok(p)) {
+        switch (k) {
+#define LFM_K(K_) case K_: return launch_band2<FAM, K_>(p, grid, st);
+        LFM_K(1) LFM_K(2) LFM_K(3) LFM_K(4) LFM_K(5) LFM_K(6) LFM_K(7)
+#undef LFM_K
+        default: return hipErrorInvalidValue;
+        }
+    }
     switch (k) {
 #define LFM_K(K_) case K_: hipLaunchKernelGGL((unpredict_band<FAM, K_>), dim3(grid), dim3(64), 0, st, p); break;
     LFM_K(1) LFM_K(2) LFM_K(3) LFM_K(4) LFM_K(5) LFM_K(6) LFM_K(7)
