@@ -4,8 +4,11 @@ One step = encode one synthetic light-field stack of the BASELINE config 3 shape
 (2048 x 2048 x 64 uint16, Nnum 15, angle family, predictor auto-selected on
 frame 0) from HBM-resident input to a complete in-memory .lfm: GPU selection
 (8 candidates, 2D entropy) + fused predictor/symbolize kernel over all 64 frames
-+ one D2H copy of the symbols + bzip2 of the 96x96x8 blocks on the host cores
-+ in-order assembly.  Nothing is cached between steps.
++ GPU bzip2 of the 3 872 96x96x8 blocks (byte-identical to libbzip2) + D2H of
+the compressed blocks into the pinned .lfm buffer, in order.  Nothing is cached
+between steps.  After the timed steps (N=1) the last .lfm is decoded once
+(host libbz2 + GPU inverse predictor) and compared with the input: `decode`
+in the JSON line, for information (not the metric).
 
 Multi-GPU (torchrun, one process per GPU): rank r encodes z-slab r of a
 (world x 64)-frame stack (lfm.shard: slabs are whole blocks deep, so the slab
@@ -105,6 +108,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frames", type=int, default=Z)
+    ap.add_argument("--no-decode", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,6 +209,15 @@ def main():
         "chosen_predictor": stats[-1]["chosen"],
         "ratio": round(px_rank * 2 / out_len, 4),
     }
+    if rank == 0 and world == 1 and not args.no_decode:
+        buf = bytes(b)
+        t1 = time.perf_counter()
+        img = lfm.decode(buf, num_threads=threads)
+        dms = (time.perf_counter() - t1) * 1e3
+        ref = d_img.cpu().numpy().view(np.uint16)
+        line["decode"] = {"ms": round(dms, 1), "Mpixel_per_s": round(px_rank / dms / 1e3, 1),
+                          "exact": bool(np.array_equal(img.reshape(ref.shape), ref)),
+                          "path": "host libbz2 on %d threads + GPU inverse predictor" % threads}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)
     if rank == 0:
