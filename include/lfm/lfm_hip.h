@@ -81,6 +81,26 @@ int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], const uint32
                          uint32_t first, uint32_t count, uint32_t level, void* d_ws, size_t ws_bytes,
                          void* d_payload, uint64_t* h_sizes, uint32_t* h_flags, void* stream);
 
+/* GPU bzip2 decode of `count` single-block streams (the .lfm block payloads,
+ * SURVEY.md 8(f2); replaces the per-block BZ2_bzBuffToBuffDecompress of
+ * klb_imageIO.cpp:1748-1821).  d_payload: device copy of the payload, 4-byte
+ * aligned, readable 8 bytes past its end; stream i is h_offs[i] .. h_offs[i+1]
+ * (host array of count + 1 byte offsets) and decodes into d_out + i *
+ * out_stride.  h_lens[i] = decoded bytes; h_flags[i]: 0 ok, 1 decode this
+ * stream with the host library (several blocks, randomised, malformed,
+ * larger than out_stride), 2 block CRC mismatch.  d_ws:
+ * lfm_hip_bunzip2_workspace_bytes(count, out_stride).  Synchronous. */
+size_t lfm_hip_bunzip2_workspace_bytes(uint32_t count, uint32_t out_stride);
+int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_offs, uint32_t count, void* d_out,
+                           uint32_t out_stride, void* d_ws, size_t ws_bytes, uint32_t* h_lens, uint32_t* h_flags,
+                           void* stream);
+
+/* Decoded blocks first .. first + count - 1 (block i at d_blocks + (i -
+ * first) * stride, x fastest) back into the device image (the inverse of the
+ * writer's block gather, klb_imageIO.cpp:133-140).  Asynchronous. */
+int lfm_hip_scatter_blocks(const void* d_blocks, uint32_t stride, uint32_t first, uint32_t count,
+                           const uint32_t dims[5], const uint32_t bs[5], uint32_t bpp, void* d_img, void* stream);
+
 /* Synthetic light-field stack of SURVEY.md 8(d) (integer generator) written
  * straight into device memory: X*Y*Z pixels of volume (c, t) = (0, t_index),
  * global pixel index offset idx0 (for z-slabs of a larger stack). */

@@ -1,0 +1,725 @@
+// lfm_bunzip2.hip -- GPU decode of the .lfm block streams (bzip2, one block per
+// stream) on gfx950: the decode side of SURVEY.md 8(f2).
+//
+// The reference decodes every block with libbzip2 on the host
+// (klb_imageIO.cpp:1748-1821 via BZ2_bzBuffToBuffDecompress); here a batch of
+// streams is decoded on the device, restating bzip2-1.0.6's decompress.c:
+//
+//   bzd_huff    one lane per stream: stream / block headers, the mapping
+//               table, selectors (unary MTF), delta-coded code lengths, the
+//               decode tables (a 10-bit lookup table per Huffman table plus
+//               limit / base / perm for longer codes, BZ2_hbCreateDecodeTables),
+//               then the symbols: RUNA/RUNB runs and move-to-front (the list
+//               of each lane in LDS, interleaved), giving the BWT last column
+//               ll[] and the block length n.  Anything else (several blocks,
+//               randomised blocks, a malformed stream) is flagged for the host.
+//   bzd_tt      one workgroup per stream: byte counts, then LF(i) = C[ll[i]] +
+//               Occ(ll[i], i) (ranks among equal bytes by 8-ballot matches,
+//               stable), tt[LF(i)] = i << 8 | ll[LF(i)] (decompress.c's fast
+//               tt), and the inverse BWT as a parallel walk: markers every kMark
+//               nodes of the cycle (plus its start, tt[origPtr] >> 8), each
+//               walker follows tt from its marker to the next one and counts,
+//               one lane chains the segments to their output offsets, the
+//               walkers walk again and write the RLE1 text.
+//   bzd_rle1    one lane per stream: RLE1 decode (4 equal bytes + a count) into
+//               the output block, CRC-32 of the block checked against the header.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+#include "lfm_hip.h"
+
+namespace lfm {
+namespace bzd {
+
+constexpr int kMaxGroups = 6;
+constexpr int kMaxAlpha = 258;
+constexpr int kMaxSel = 18002;
+constexpr int kMaxLen = 20;
+constexpr int kLutBits = 10;
+constexpr uint32_t kMark = 128;  // cycle nodes per inverse-BWT walker (on average)
+
+// flags
+constexpr uint32_t kHost = 1;      // decode with the host library
+constexpr uint32_t kCrcFail = 2;   // decoded, but the block CRC does not match
+
+__constant__ uint32_t c_dcrc[256];
+
+struct Dec {
+    const uint8_t* payload;   // 4-byte aligned
+    const uint64_t* offs;     // count + 1 byte offsets
+    uint32_t count;
+    uint32_t cap;             // RLE1 / ll capacity per stream
+    uint32_t out_stride;
+    uint8_t* out;
+    uint8_t* ll;              // cap per stream
+    uint32_t* tt;             // cap per stream
+    uint8_t* rle;             // cap per stream
+    uint16_t* lut;            // kMaxGroups << kLutBits per stream
+    int32_t* limit;           // kMaxGroups * (kMaxLen + 2) per stream
+    int32_t* base;            // kMaxGroups * (kMaxLen + 2) per stream
+    uint16_t* perm;           // kMaxGroups * kMaxAlpha per stream
+    uint8_t* sel;             // kMaxSel per stream
+    uint32_t mcap;            // markers per stream
+    uint32_t* mnext;
+    uint32_t* mlen;
+    uint32_t* mstart;
+    uint32_t* n;
+    uint32_t* orig;
+    uint32_t* crc;
+    uint32_t* flags;
+    uint32_t* out_len;
+    uint32_t* minlen;         // kMaxGroups per stream (min code length)
+};
+
+// MSB-first bit reader over the payload: a 64-bit window of two big-endian
+// words, refilled one aligned word at a time.
+struct BitReader {
+    const uint32_t* w;
+    uint64_t pos;    // absolute bit position
+    uint64_t wpos;   // word index of the window's first word
+    uint64_t win;
+    uint64_t end;    // bit position past the stream
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return __builtin_bswap32(w[i]); }
+    __device__ __forceinline__ void init(const uint8_t* payload, uint64_t byte0, uint64_t byte1)
+    {
+        w = (const uint32_t*)payload;
+        pos = byte0 * 8;
+        end = byte1 * 8;
+        wpos = pos >> 5;
+        win = ((uint64_t)word(wpos) << 32) | word(wpos + 1);
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t nb) const  // nb in 1..32
+    {
+        const uint32_t off = (uint32_t)(pos - 32 * wpos);
+        return (uint32_t)((win << off) >> (64 - nb));
+    }
+    __device__ __forceinline__ void skip(uint32_t nb)
+    {
+        pos += nb;
+        while (pos - 32 * wpos >= 32) {
+            ++wpos;
+            win = (win << 32) | word(wpos + 1);
+        }
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t nb)
+    {
+        const uint32_t v = peek(nb);
+        skip(nb);
+        return v;
+    }
+    __device__ __forceinline__ bool over() const { return pos > end; }
+};
+
+// ----------------------------------------------------------------- huffman --
+// One wave per stream.  The decode is one sequential chain per stream, so
+// every lane runs the same (wave-uniform) header and symbol code; what the
+// wave buys is storage and wide steps:
+//  * the decode tables live in LDS (a 10-bit lookup table per Huffman table:
+//    one broadcast LDS read decodes most symbols);
+//  * the move-to-front list and seqToUnseq are registers, 4 entries per lane:
+//    a move-to-front of position m is one lane shift and a byte select, not m
+//    serial moves; list[m] is one readlane;
+//  * the bit window is refilled from a 4-word lookahead queue, so the load of
+//    a payload word is issued ~4 refills before it is needed;
+//  * a RUNA/RUNB run is written by all 64 lanes.
+// Output: the BWT last column ll[], n, origPtr, the block CRC.
+struct WaveBits {
+    const uint32_t* w;
+    uint64_t pos, wpos, end;
+    uint64_t win;
+    uint32_t q0, q1, q2, q3;  // words wpos + 2 .. wpos + 5
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return __builtin_bswap32(w[i]); }
+    __device__ __forceinline__ void init(const uint8_t* payload, uint64_t byte0, uint64_t byte1)
+    {
+        w = (const uint32_t*)payload;
+        pos = byte0 * 8;
+        end = byte1 * 8;
+        wpos = pos >> 5;
+        win = ((uint64_t)word(wpos) << 32) | word(wpos + 1);
+        q0 = word(wpos + 2);
+        q1 = word(wpos + 3);
+        q2 = word(wpos + 4);
+        q3 = word(wpos + 5);
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t nb) const
+    {
+        const uint32_t off = (uint32_t)(pos - 32 * wpos);
+        return (uint32_t)((win << off) >> (64 - nb));
+    }
+    __device__ __forceinline__ void skip(uint32_t nb)
+    {
+        pos += nb;
+        while (pos - 32 * wpos >= 32) {
+            ++wpos;
+            win = (win << 32) | q0;
+            q0 = q1;
+            q1 = q2;
+            q2 = q3;
+            q3 = pos < end + 64 ? word(wpos + 5) : 0u;  // never past the payload's slack
+        }
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t nb)
+    {
+        const uint32_t v = peek(nb);
+        skip(nb);
+        return v;
+    }
+    __device__ __forceinline__ bool over() const { return pos > end; }
+};
+
+__device__ __forceinline__ uint32_t lane_byte(uint32_t w4, uint32_t idx)  // entry idx of a 4-per-lane list
+{
+    return (__builtin_amdgcn_readlane(w4, idx >> 2) >> (8 * (idx & 3))) & 0xFFu;
+}
+
+__global__ __launch_bounds__(64) void bzd_huff(Dec D)
+{
+    __shared__ uint16_t lut[kMaxGroups << kLutBits];
+    __shared__ int32_t slimit[kMaxGroups][kMaxLen + 2];
+    __shared__ int32_t sbase[kMaxGroups][kMaxLen + 2];
+    __shared__ uint16_t sperm[kMaxGroups][kMaxAlpha];
+    __shared__ uint8_t slen[kMaxAlpha];
+    __shared__ int scnt[kMaxLen + 2], sstart[kMaxLen + 2];
+    // selectors in LDS: a uniform global load of what lane 0 just stored could
+    // be served by the (incoherent) scalar cache
+    __shared__ uint8_t sel[kMaxSel];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t s = blockIdx.x;
+    uint32_t flag = 0;
+    WaveBits br;
+    const uint64_t b0 = D.offs[s], b1 = D.offs[s + 1];
+    br.init(D.payload, b0, b1);
+    uint8_t* ll = D.ll + (size_t)s * D.cap;
+    uint32_t nblock = 0, origPtr = 0, bcrc = 0;
+    uint32_t s2u = 0;  // seqToUnseq, entries 4 * lane .. 4 * lane + 3
+    do {
+        if (b1 - b0 < 14) { flag = kHost; break; }
+        if (br.get(24) != 0x425A68u) { flag = kHost; break; }  // "BZh"
+        const uint32_t lv = br.get(8);
+        if (lv < '1' || lv > '9') { flag = kHost; break; }
+        const uint32_t m1 = br.get(24), m2 = br.get(24);
+        if (m1 != 0x314159u || m2 != 0x265359u) { flag = kHost; break; }  // no block (empty) or damaged
+        bcrc = br.get(32);
+        if (br.get(1)) { flag = kHost; break; }  // randomised block (bzip2 0.9.0 style)
+        origPtr = br.get(24);
+        // mapping table -> seqToUnseq
+        const uint32_t in16 = br.get(16);
+        uint32_t nInUse = 0;
+        for (int i = 0; i < 16; ++i)
+            if ((in16 >> (15 - i)) & 1u) {
+                const uint32_t bits = br.get(16);
+                for (int j = 0; j < 16; ++j)
+                    if ((bits >> (15 - j)) & 1u) {
+                        if ((nInUse >> 2) == lane) s2u |= (uint32_t)(i * 16 + j) << (8 * (nInUse & 3));
+                        ++nInUse;
+                    }
+            }
+        if (nInUse == 0) { flag = kHost; break; }
+        const int alphaSize = (int)nInUse + 2;
+        const int nGroups = (int)br.get(3);
+        const uint32_t nSel = br.get(15);
+        if (nGroups < 2 || nGroups > kMaxGroups || nSel < 1 || nSel > kMaxSel) { flag = kHost; break; }
+        {  // selectors: unary MTF values, then the inverse MTF
+            uint32_t pos = 0x543210u;
+            for (uint32_t i = 0; i < nSel && !flag; ++i) {
+                uint32_t j = 0;
+                while (br.get(1)) {
+                    if (++j >= (uint32_t)nGroups) { flag = kHost; break; }
+                }
+                const uint32_t v = (pos >> (4 * j)) & 15u;
+                const uint32_t m = (1u << (4 * (j + 1))) - 1u;
+                pos = (pos & ~m) | (((pos << 4) | v) & m);
+                if (lane == 0) sel[i] = (uint8_t)v;
+            }
+            if (flag) break;
+        }
+        __syncthreads();
+        // code lengths and decode tables (BZ2_hbCreateDecodeTables, restated)
+        for (int t = 0; t < nGroups && !flag; ++t) {
+            int curr = (int)br.get(5);
+            int mn = 32, mx = 0;
+            for (int i = 0; i < alphaSize; ++i) {
+                while (true) {
+                    if (curr < 1 || curr > kMaxLen) { flag = kHost; break; }
+                    if (!br.get(1)) break;
+                    curr += br.get(1) ? -1 : 1;
+                }
+                if (flag) break;
+                if (lane == 0) slen[i] = (uint8_t)curr;
+                mn = min(mn, curr);
+                mx = max(mx, curr);
+            }
+            if (flag) break;
+            __syncthreads();
+            if (lane == 0) {
+                for (int l = 0; l < kMaxLen + 2; ++l) scnt[l] = 0;
+                for (int i = 0; i < alphaSize; ++i) ++scnt[slen[i]];
+                int pp = 0;
+                for (int l = 0; l < kMaxLen + 2; ++l) {
+                    sstart[l] = pp;
+                    pp += scnt[l];
+                }
+                for (int i = 0; i < alphaSize; ++i) sperm[t][sstart[slen[i]]++] = (uint16_t)i;
+                int vec = 0, firstIdx = 0;
+                for (int l = 0; l < kMaxLen + 2; ++l) {
+                    if (l < mn || l > mx) {
+                        slimit[t][l] = l < mn ? -1 : 0x7FFFFFFF;
+                        sbase[t][l] = 0;
+                        continue;
+                    }
+                    sbase[t][l] = vec - firstIdx;  // code vec has perm index firstIdx
+                    vec += scnt[l];
+                    firstIdx += scnt[l];
+                    slimit[t][l] = vec - 1;
+                    vec <<= 1;
+                }
+            }
+            __syncthreads();
+            // lookup table: entry = sym + 1 (0: longer code) | length << 9
+            uint16_t* lt = lut + (t << kLutBits);
+            for (int e = lane; e < (1 << kLutBits); e += 64) {
+                uint16_t ent = 0;
+                for (int l = mn; l <= min(mx, kLutBits); ++l) {
+                    const int c = e >> (kLutBits - l);  // the first l bits of e
+                    if (c <= slimit[t][l] && c > slimit[t][l] - scnt[l]) {
+                        ent = (uint16_t)((sperm[t][c - sbase[t][l]] + 1) | (l << 9));
+                        break;
+                    }
+                }
+                lt[e] = ent;
+            }
+            __syncthreads();
+        }
+        if (flag) break;
+        // symbols
+        uint32_t mtfw = (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
+        const uint32_t EOB = nInUse + 1;
+        int groupNo = -1, groupPos = 0, t = 0;
+        uint32_t next_t = sel[0];
+        auto next_sym = [&]() -> int {
+            if (groupPos == 0) {
+                ++groupNo;
+                if ((uint32_t)groupNo >= nSel) return -1;
+                groupPos = 50;
+                t = (int)next_t;
+                next_t = (uint32_t)groupNo + 1 < nSel ? sel[groupNo + 1] : 0u;  // one group ahead
+            }
+            --groupPos;
+            const uint32_t e = lut[(t << kLutBits) + br.peek(kLutBits)];
+            if (e) {
+                br.skip(e >> 9);
+                return (int)(e & 511u) - 1;
+            }
+            int zn = kLutBits + 1;  // longer than kLutBits: bzip2's limit walk
+            int32_t zvec = (int32_t)br.peek(zn);
+            while (zn <= kMaxLen && zvec > slimit[t][zn]) {
+                ++zn;
+                zvec = (int32_t)br.peek(zn);
+            }
+            if (zn > kMaxLen) return -1;
+            br.skip(zn);
+            const int idx = zvec - sbase[t][zn];
+            if (idx < 0 || idx >= alphaSize) return -1;
+            return sperm[t][idx];
+        };
+        const uint32_t cap = D.cap;
+        int sym = next_sym();
+        while (true) {
+            if (sym < 0 || br.over()) { flag = kHost; break; }
+            if ((uint32_t)sym == EOB) break;
+            if (sym <= 1) {  // RUNA / RUNB: a run of the list front
+                uint32_t es = 0, N = 1;
+                do {
+                    es += (uint32_t)(sym + 1) * N;
+                    N <<= 1;
+                    if (N > (1u << 21)) { flag = kHost; break; }
+                    sym = next_sym();
+                } while (sym >= 0 && sym <= 1);
+                if (flag) break;
+                if (nblock + es > cap) { flag = kHost; break; }
+                const uint8_t uc = (uint8_t)lane_byte(s2u, lane_byte(mtfw, 0));
+                for (uint32_t k = lane; k < es; k += 64) ll[nblock + k] = uc;
+                nblock += es;
+                continue;  // sym already holds the next symbol
+            }
+            if (nblock >= cap) { flag = kHost; break; }
+            const uint32_t nn = (uint32_t)sym - 1;
+            const uint32_t v = lane_byte(mtfw, nn);
+            // move to front: entries 0 .. nn shift up by one, v goes to 0
+            uint32_t up = __shfl_up(mtfw, 1);
+            if (lane == 0) up = v << 24;
+            const uint32_t sh = (mtfw << 8) | (up >> 24);
+            const int k = min(4, max(0, (int)nn - 4 * (int)lane + 1));  // entries of this lane at <= nn
+            const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+            mtfw = (sh & msk) | (mtfw & ~msk);
+            if (lane == 0) ll[nblock] = (uint8_t)lane_byte(s2u, v);
+            ++nblock;
+            sym = next_sym();
+        }
+        if (flag) break;
+        if (origPtr >= nblock || nblock == 0) { flag = kHost; break; }
+        // end of stream: exactly one block
+        const uint32_t e1 = br.get(24), e2 = br.get(24);
+        if (e1 != 0x177245u || e2 != 0x385090u) { flag = kHost; break; }
+        const uint32_t ccrc = br.get(32);
+        if (ccrc != bcrc) { flag = kHost; break; }  // one block: combined CRC = rotl(0, 1) ^ blockCRC
+    } while (false);
+    if (lane == 0) {
+        D.flags[s] = flag;
+        D.n[s] = flag ? 0u : nblock;
+        D.orig[s] = origPtr;
+        D.crc[s] = bcrc;
+    }
+}
+
+// ------------------------------------------------------------ inverse BWT --
+constexpr int kTtThreads = 256;
+
+__global__ __launch_bounds__(kTtThreads) void bzd_tt(Dec D)
+{
+    __shared__ uint32_t cf[256];       // C[c]: bytes < c
+    __shared__ uint32_t run[256];      // occurrences of c before the current tile
+    __shared__ uint32_t wc[kTtThreads / 64][256];
+    const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (D.flags[s]) return;
+    const uint32_t n = D.n[s];
+    const uint8_t* ll = D.ll + (size_t)s * D.cap;
+    uint32_t* tt = D.tt + (size_t)s * D.cap;
+    for (uint32_t c = t; c < 256; c += kTtThreads) {
+        run[c] = 0;
+        for (int w = 0; w < kTtThreads / 64; ++w) wc[w][c] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += kTtThreads) atomicAdd(&run[ll[i]], 1u);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of the 256 counts, 4 per lane
+        uint32_t v[4], sum = 0;
+        for (int q = 0; q < 4; ++q) {
+            v[q] = run[4 * t + q];
+            sum += v[q];
+        }
+        uint32_t inc = sum;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d);
+            if ((int)t >= d) inc += o;
+        }
+        uint32_t acc = inc - sum;
+        for (int q = 0; q < 4; ++q) {
+            cf[4 * t + q] = acc;
+            acc += v[q];
+        }
+    }
+    __syncthreads();
+    for (uint32_t c = t; c < 256; c += kTtThreads) run[c] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // LF(i) = C[c] + Occ(c, i) in tiles of kTtThreads positions
+    for (uint32_t i0 = 0; i0 < n; i0 += kTtThreads) {
+        const uint32_t i = i0 + t;
+        const bool ok = i < n;
+        const uint32_t c = ok ? ll[i] : 256u;
+        uint64_t mm = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t bb = __ballot(ok && ((c >> b) & 1u));
+            mm &= ((c >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rw = (uint32_t)__popcll(mm & lt);
+        const bool leader = ok && (mm & lt) == 0;
+        if (leader) wc[wave][c] = (uint32_t)__popcll(mm);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        if (ok) {
+            for (uint32_t w = 0; w < kTtThreads / 64; ++w) {
+                const uint32_t x = wc[w][c];
+                before += w < wave ? x : 0u;
+                total += x;
+            }
+            const uint32_t lf = cf[c] + run[c] + before + rw;
+            tt[lf] = i;
+        }
+        __syncthreads();
+        // the last occurrence of c in the tile advances the running count
+        if (ok && before + rw + 1 == total) run[c] += total;
+        if (leader) wc[wave][c] = 0;
+        __syncthreads();
+    }
+    __syncthreads();
+    // decompress.c's fast tt: tt[j] = next << 8 | ll[j]
+    for (uint32_t j = t; j < n; j += kTtThreads) tt[j] = (tt[j] << 8) | ll[j];
+}
+
+// marker id of node j (or ~0u): every kMark-th node, and the walk's start
+__device__ __forceinline__ uint32_t marker_id(uint32_t j, uint32_t v0, uint32_t nm)
+{
+    if (j % kMark == 0) return j / kMark;
+    return j == v0 ? nm : ~0u;
+}
+
+__global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
+{
+    __shared__ uint32_t s_total;
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (D.flags[s]) return;
+    const uint32_t n = D.n[s];
+    const uint32_t* tt = D.tt + (size_t)s * D.cap;
+    uint8_t* rle = D.rle + (size_t)s * D.cap;
+    uint32_t* mnext = D.mnext + (size_t)s * D.mcap;
+    uint32_t* mlen = D.mlen + (size_t)s * D.mcap;
+    uint32_t* mstart = D.mstart + (size_t)s * D.mcap;
+    const uint32_t v0 = tt[D.orig[s]] >> 8;
+    const uint32_t nm = (n + kMark - 1) / kMark;  // regular markers 0 .. nm-1, the start is nm
+    const bool extra = (v0 % kMark) != 0;
+    const uint32_t nwalk = nm + (extra ? 1u : 0u);
+    auto node_of = [&](uint32_t id) { return id < nm ? id * kMark : v0; };
+    // pass 1: segment lengths and successors
+    for (uint32_t id = t; id < nwalk; id += kTtThreads) {
+        uint32_t pos = node_of(id), len = 0, nx = ~0u;
+        do {
+            pos = tt[pos] >> 8;
+            ++len;
+            nx = marker_id(pos, v0, nm);
+        } while (nx == ~0u && len <= n);
+        mnext[id] = nx;
+        mlen[id] = len;
+    }
+    __syncthreads();
+    // chain the segments from the start (one lane)
+    if (t == 0) {
+        uint32_t id = extra ? nm : v0 / kMark, off = 0, k = 0;
+        while (k < nwalk && off < n) {
+            mstart[id] = off;
+            off += mlen[id];
+            id = mnext[id];
+            ++k;
+        }
+        s_total = off == n && k == nwalk ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_total) {
+        if (t == 0) D.flags[s] = kHost;  // not one cycle: not a valid bzip2 block
+        return;
+    }
+    // pass 2: the RLE1 text, segment by segment
+    for (uint32_t id = t; id < nwalk; id += kTtThreads) {
+        uint32_t pos = node_of(id), o = mstart[id];
+        const uint32_t len = mlen[id];
+        for (uint32_t k = 0; k < len; ++k) {
+            const uint32_t e = tt[pos];
+            rle[o + k] = (uint8_t)e;
+            pos = e >> 8;
+        }
+    }
+}
+
+// -------------------------------------------------------------------- RLE1 --
+__global__ __launch_bounds__(64) void bzd_rle1(Dec D)
+{
+    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+    if (s >= D.count) return;
+    if (D.flags[s]) {
+        D.out_len[s] = 0;
+        return;
+    }
+    const uint32_t n = D.n[s];
+    const uint8_t* rle = D.rle + (size_t)s * D.cap;
+    uint8_t* out = D.out + (size_t)s * D.out_stride;
+    const uint32_t cap = D.out_stride;
+    uint32_t o = 0, crc = 0xffffffffu, prev = 256, cnt = 0;
+    bool bad = false;
+    auto put = [&](uint32_t b) {
+        if (o < cap) out[o] = (uint8_t)b;
+        ++o;
+        crc = (crc << 8) ^ c_dcrc[(crc >> 24) ^ b];
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t b = rle[i];
+        if (cnt == 4) {  // the count byte after 4 equal bytes
+            for (uint32_t k = 0; k < b; ++k) put(prev);
+            cnt = 0;
+            prev = 256;
+            continue;
+        }
+        put(b);
+        if (b == prev) ++cnt;
+        else {
+            prev = b;
+            cnt = 1;
+        }
+    }
+    if (o > cap) bad = true;
+    crc = ~crc;
+    D.out_len[s] = o;
+    if (bad) D.flags[s] = kHost;
+    else if (crc != D.crc[s]) D.flags[s] = kCrcFail;
+}
+
+} // namespace bzd
+} // namespace lfm
+
+using namespace lfm::bzd;
+
+namespace {
+
+size_t al(size_t v) { return (v + 255) / 256 * 256; }
+
+uint32_t dec_cap(uint32_t out_stride)
+{
+    // a .lfm block of B bytes is compressed at level min(9, ceil(B / 1e5))
+    // (klb_imageIO.cpp:108): its RLE1 block is at most 100000 * level bytes
+    const uint32_t level = std::min<uint32_t>(9, std::max<uint32_t>(1, (out_stride + 99999) / 100000));
+    return (uint32_t)al(100000u * level + 64);
+}
+
+uint32_t mark_cap(uint32_t cap) { return (cap + kMark - 1) / kMark + 2; }
+
+uint32_t host_dcrc[256];
+bool dcrc_ready = false;
+
+} // namespace
+
+extern "C" size_t lfm_hip_bunzip2_workspace_bytes(uint32_t count, uint32_t out_stride)
+{
+    const size_t cap = dec_cap(out_stride), mc = mark_cap((uint32_t)cap);
+    size_t b = 0;
+    b += al(((size_t)count + 1) * 8);
+    b += al((size_t)count * cap);          // ll
+    b += al((size_t)count * cap * 4);      // tt
+    b += al((size_t)count * cap);          // rle
+    b += al((size_t)count * (kMaxGroups << kLutBits) * 2);
+    b += 2 * al((size_t)count * kMaxGroups * (kMaxLen + 2) * 4);
+    b += al((size_t)count * kMaxGroups * kMaxAlpha * 2);
+    b += al((size_t)count * kMaxSel);
+    b += 3 * al((size_t)count * mc * 4);
+    b += 6 * al((size_t)count * 4 + 64);
+    b += al((size_t)count * kMaxGroups * 4);
+    return b;
+}
+
+// Decode streams [0, count) of the device payload (byte ranges h_offs[i] ..
+// h_offs[i + 1]; the payload buffer must be 4-byte aligned and readable 8 bytes
+// past its end) into d_out + i * out_stride.  h_lens[i] = decoded bytes,
+// h_flags[i]: 0 ok, 1 decode with the host library, 2 CRC mismatch.
+extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_offs, uint32_t count, void* d_out,
+                                      uint32_t out_stride, void* d_ws, size_t ws_bytes, uint32_t* h_lens,
+                                      uint32_t* h_flags, void* stream_)
+{
+    hipStream_t st = (hipStream_t)stream_;
+    if (!d_payload || !h_offs || !count || !d_out || !out_stride || !d_ws) return LFM_HIP_EINVAL;
+    if (ws_bytes < lfm_hip_bunzip2_workspace_bytes(count, out_stride) || ((uintptr_t)d_payload & 3)) return LFM_HIP_EINVAL;
+    if (!dcrc_ready) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t c = i << 24;
+            for (int k = 0; k < 8; ++k) c = (c & 0x80000000u) ? (c << 1) ^ 0x04c11db7u : (c << 1);
+            host_dcrc[i] = c;
+        }
+        dcrc_ready = true;
+    }
+    static thread_local int crc_dev = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (crc_dev != dev) {
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_dcrc), host_dcrc, sizeof(host_dcrc)) != hipSuccess) return LFM_HIP_ERUNTIME;
+        crc_dev = dev;
+    }
+    Dec D{};
+    D.payload = (const uint8_t*)d_payload;
+    D.count = count;
+    D.cap = dec_cap(out_stride);
+    D.mcap = mark_cap(D.cap);
+    D.out_stride = out_stride;
+    D.out = (uint8_t*)d_out;
+    uint8_t* p = (uint8_t*)d_ws;
+    auto take = [&](size_t bytes) { uint8_t* r = p; p += al(bytes); return r; };
+    uint64_t* d_offs = (uint64_t*)take(((size_t)count + 1) * 8);
+    D.offs = d_offs;
+    D.ll = take((size_t)count * D.cap);
+    D.tt = (uint32_t*)take((size_t)count * D.cap * 4);
+    D.rle = take((size_t)count * D.cap);
+    D.lut = (uint16_t*)take((size_t)count * (kMaxGroups << kLutBits) * 2);
+    D.limit = (int32_t*)take((size_t)count * kMaxGroups * (kMaxLen + 2) * 4);
+    D.base = (int32_t*)take((size_t)count * kMaxGroups * (kMaxLen + 2) * 4);
+    D.perm = (uint16_t*)take((size_t)count * kMaxGroups * kMaxAlpha * 2);
+    D.sel = take((size_t)count * kMaxSel);
+    D.mnext = (uint32_t*)take((size_t)count * D.mcap * 4);
+    D.mlen = (uint32_t*)take((size_t)count * D.mcap * 4);
+    D.mstart = (uint32_t*)take((size_t)count * D.mcap * 4);
+    uint32_t** small[] = {&D.n, &D.orig, &D.crc, &D.flags, &D.out_len};
+    for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
+    (void)take((size_t)count * 4 + 64);
+    D.minlen = (uint32_t*)take((size_t)count * kMaxGroups * 4);
+    if (hipMemcpyAsync(d_offs, h_offs, ((size_t)count + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess)
+        return LFM_HIP_ERUNTIME;
+    const uint32_t g64 = (count + 63) / 64;
+    hipLaunchKernelGGL(bzd_huff, dim3(count), dim3(64), 0, st, D);
+    hipLaunchKernelGGL(bzd_tt, dim3(count), dim3(kTtThreads), 0, st, D);
+    hipLaunchKernelGGL(bzd_walk, dim3(count), dim3(kTtThreads), 0, st, D);
+    hipLaunchKernelGGL(bzd_rle1, dim3(g64), dim3(64), 0, st, D);
+    if (hipGetLastError() != hipSuccess) return LFM_HIP_ERUNTIME;
+    if (hipMemcpyAsync(h_lens, D.out_len, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(h_flags, D.flags, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return LFM_HIP_ERUNTIME;
+    return LFM_HIP_OK;
+}
+
+// ------------------------------------------------------------ block scatter --
+namespace lfm {
+namespace bzd {
+
+struct Grid5 {
+    uint32_t dims[5], bs[5], nb[5], bpp;
+};
+
+// decoded blocks (x fastest, then y, z, c, t: the writer's gather order,
+// klb_imageIO.cpp:133-140) back into the image
+__global__ __launch_bounds__(256) void scatter_blocks(const uint8_t* __restrict__ blocks, uint32_t stride, Grid5 G,
+                                                      uint32_t first, uint8_t* __restrict__ img)
+{
+    const uint32_t s = blockIdx.y;
+    uint32_t org[5], sz[5], id = first + s;
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+        const uint32_t q = id % G.nb[d];
+        id /= G.nb[d];
+        org[d] = q * G.bs[d];
+        sz[d] = min(G.bs[d], G.dims[d] - org[d]);
+    }
+    const uint32_t rowb = sz[0] * G.bpp;
+    const uint32_t nrows = sz[1] * sz[2] * sz[3] * sz[4];
+    const uint8_t* src = blocks + (size_t)s * stride;
+    for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+        uint32_t q = r;
+        const uint32_t y = q % sz[1]; q /= sz[1];
+        const uint32_t z = q % sz[2]; q /= sz[2];
+        const uint32_t c = q % sz[3]; q /= sz[3];
+        const size_t dst = ((((size_t)(org[4] + q) * G.dims[3] + (org[3] + c)) * G.dims[2] + (org[2] + z)) *
+                                G.dims[1] + (org[1] + y)) * G.dims[0] + org[0];
+        uint8_t* dp = img + dst * G.bpp;
+        const uint8_t* sp = src + (size_t)r * rowb;
+        for (uint32_t i = threadIdx.x; i < rowb; i += blockDim.x) dp[i] = sp[i];
+    }
+}
+
+} // namespace bzd
+} // namespace lfm
+
+extern "C" int lfm_hip_scatter_blocks(const void* d_blocks, uint32_t stride, uint32_t first, uint32_t count,
+                                      const uint32_t dims[5], const uint32_t bs[5], uint32_t bpp, void* d_img,
+                                      void* stream_)
+{
+    if (!d_blocks || !d_img || !count || !bpp) return LFM_HIP_EINVAL;
+    lfm::bzd::Grid5 G;
+    for (int d = 0; d < 5; ++d) {
+        if (!dims[d] || !bs[d]) return LFM_HIP_EINVAL;
+        G.dims[d] = dims[d];
+        G.bs[d] = bs[d];
+        G.nb[d] = (dims[d] + bs[d] - 1) / bs[d];
+    }
+    G.bpp = bpp;
+    hipLaunchKernelGGL(lfm::bzd::scatter_blocks, dim3(64, count), dim3(256), 0, (hipStream_t)stream_,
+                       (const uint8_t*)d_blocks, stride, G, first, (uint8_t*)d_img);
+    return hipGetLastError() == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
+}

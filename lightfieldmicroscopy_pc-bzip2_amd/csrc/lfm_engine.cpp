@@ -360,6 +360,13 @@ bool gpu_bzip2_enabled()
     return on;
 }
 
+// the GPU bzip2 decoder (env LFM_GPU_BUNZIP2=0: host libbz2 per block)
+bool gpu_bunzip2_enabled()
+{
+    static const bool on = env_int("LFM_GPU_BUNZIP2", 1) != 0;
+    return on;
+}
+
 Encoder::Encoder(int device) : device_(device) {}
 
 Encoder::~Encoder()
@@ -981,6 +988,107 @@ void parallel_for(uint64_t n, int threads, F&& f)
 }
 } // namespace
 
+// GPU decode of a BZIP2 payload (lfm_bunzip2.hip): payload up, streams decoded
+// in batches into the device image (the few flagged streams by the host
+// library), inverse predictor on the device, image down.  Returns -1 when the
+// GPU path does not apply (the caller decodes on the host).
+static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int family,
+                      bool predicted, int k, int video)
+{
+    const BlockGrid g(h);
+    const uint64_t nb = g.nblocks;
+    const size_t bpp = h.getBytesPerPixel();
+    const uint32_t block_bytes = h.getBlockSizeBytes();
+    if (!nb || !block_bytes || nb >= (1ull << 31)) return -1;
+    std::vector<uint64_t> offs(nb + 1);
+    for (uint64_t i = 0; i < nb; ++i) {
+        offs[i] = h.getBlockOffset(i);
+        if (i && offs[i] != offs[i - 1] + h.getBlockCompressedSizeBytes(i - 1)) return -1;  // not contiguous
+    }
+    offs[nb] = offs[nb - 1] + h.getBlockCompressedSizeBytes(nb - 1);
+    if (offs[nb] > len) return 3;
+    const size_t img_bytes = h.getImageSizeBytes();
+    const size_t per = lfm_hip_bunzip2_workspace_bytes(1, block_bytes) + block_bytes;
+    const size_t budget = (size_t)env_int("LFM_BUNZIP2_GPU_BUDGET_MB", 16 * 1024) << 20;
+    const uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nb, budget / per));
+    const size_t ws = lfm_hip_bunzip2_workspace_bytes((uint32_t)batch, block_bytes);
+    hipStream_t st = nullptr;
+    void *d_pay = nullptr, *d_ws = nullptr, *d_blk = nullptr, *d_sym = nullptr, *d_out = nullptr;
+    auto release = [&]() {
+        for (void* q : {d_pay, d_ws, d_blk, d_sym, d_out})
+            if (q) (void)hipFree(q);
+        if (st) (void)hipStreamDestroy(st);
+    };
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipMalloc(&d_pay, offs[nb] + 64) != hipSuccess ||
+        hipMalloc(&d_ws, ws) != hipSuccess || hipMalloc(&d_blk, batch * block_bytes) != hipSuccess ||
+        hipMalloc(&d_sym, img_bytes) != hipSuccess || (predicted && hipMalloc(&d_out, img_bytes) != hipSuccess)) {
+        (void)hipGetLastError();
+        release();
+        return -1;
+    }
+    int rc = 0;
+    if (hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, st) != hipSuccess)
+        rc = 3;
+    uint32_t dims[5], bs[5];
+    for (int d = 0; d < 5; ++d) {
+        dims[d] = h.xyzct[d];
+        bs[d] = (uint32_t)g.bs[d];
+    }
+    std::vector<uint32_t> lens(batch), flags(batch);
+    std::vector<uint8_t> hb(block_bytes);
+    for (uint64_t b0 = 0; b0 < nb && !rc; b0 += batch) {
+        const uint32_t cnt = (uint32_t)std::min<uint64_t>(batch, nb - b0);
+        if (lfm_hip_bunzip2_blocks(d_pay, offs.data() + b0, cnt, d_blk, block_bytes, d_ws, ws, lens.data(),
+                                   flags.data(), st) != LFM_HIP_OK) {
+            rc = 3;
+            break;
+        }
+        for (uint32_t i = 0; i < cnt && !rc; ++i) {
+            uint64_t o[5], sz[5];
+            g.block(b0 + i, o, sz);
+            const uint64_t expect = bpp * sz[0] * sz[1] * sz[2] * sz[3] * sz[4];
+            if (flags[i] == 1) {  // the host library decodes this stream
+                const int r = decompress_one(BZIP2, payload + offs[b0 + i], (uint32_t)(offs[b0 + i + 1] - offs[b0 + i]),
+                                             hb.data(), (uint32_t)expect);
+                if (r) rc = r;
+                else if (hipMemcpyAsync((uint8_t*)d_blk + (size_t)i * block_bytes, hb.data(), expect,
+                                        hipMemcpyHostToDevice, st) != hipSuccess ||
+                         hipStreamSynchronize(st) != hipSuccess)
+                    rc = 3;
+            } else if (flags[i] != 0 || lens[i] != expect) {
+                std::printf("ERROR: block %llu of the payload does not decode to its %llu bytes (bzip2 CRC / length)\n",
+                            (unsigned long long)(b0 + i), (unsigned long long)expect);
+                rc = 2;
+            }
+        }
+        if (!rc && lfm_hip_scatter_blocks(d_blk, block_bytes, (uint32_t)b0, cnt, dims, bs, (uint32_t)bpp, d_sym, st) !=
+                       LFM_HIP_OK)
+            rc = 3;
+    }
+    if (!rc && predicted) {
+        const int W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
+        const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
+        const size_t vb = (size_t)W * H * Z * 2;
+        for (uint64_t v = 0; v < V && !rc; ++v) {
+            const int hr = lfm_hip_unpredict((const uint16_t*)((uint8_t*)d_sym + v * vb), nullptr,
+                                             (uint16_t*)((uint8_t*)d_out + v * vb), W, H, Z, h.Nnum, family, k, video,
+                                             0, st);
+            if (hr == LFM_HIP_ENOTINV) {
+                std::printf("ERROR: frames of this file cannot be inverted (temporal angle/space predictor)\n");
+                rc = 3;
+            } else if (hr != LFM_HIP_OK) {
+                rc = 3;
+            }
+        }
+    }
+    if (!rc && (hipMemcpyAsync(img, predicted ? d_out : d_sym, img_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+        rc = 3;
+    release();
+    return rc;
+}
+
 int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int threads,
                    int family)
 {
@@ -995,6 +1103,11 @@ int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h
     if (predicted && (k > 7 || h.Nnum == 0)) {
         std::printf("ERROR: unknown predictor %d in header\n", k);
         return 3;
+    }
+    if (h.compressionType == BZIP2 && gpu_decode_enabled() && gpu_bunzip2_enabled() && lfm_hip_device_count() > 0 &&
+        (!predicted || h.Nnum <= 31)) {
+        const int rc = gpu_decode(payload, len, h, img, family, predicted, k, video);
+        if (rc != -1) return rc;
     }
     std::vector<uint16_t> symbuf;
     uint8_t* sym = img;

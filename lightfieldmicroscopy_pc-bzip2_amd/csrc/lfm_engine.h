@@ -18,6 +18,7 @@ constexpr int kErrNoGpu = 7;
 
 bool gpu_bzip2_enabled();   // env LFM_GPU_BZIP2 (default on)
 bool gpu_decode_enabled();  // env LFM_GPU_DECODE (default on): inverse predictor on the GPU
+bool gpu_bunzip2_enabled(); // env LFM_GPU_BUNZIP2 (default on): bzip2 decode on the GPU
 int default_threads();      // env LFM_NUM_THREADS, else OMP_NUM_THREADS, else hardware_concurrency
 int current_family();       // lfm_set_family / env LFM_PREDICTOR_WAY / LFM_PREDICTOR_WAY
 void set_family(int fam);
