@@ -7,7 +7,7 @@ frame 0) from HBM-resident input to a complete in-memory .lfm: GPU selection
 + GPU bzip2 of the 3 872 96x96x8 blocks (byte-identical to libbzip2) + D2H of
 the compressed blocks into the pinned .lfm buffer, in order.  Nothing is cached
 between steps.  After the timed steps (N=1) the last .lfm is decoded once
-(host libbz2 + GPU inverse predictor) and compared with the input: `decode`
+(GPU bzip2 decode + GPU inverse predictor) and compared with the input: `decode`
 in the JSON line, for information (not the metric).
 
 Multi-GPU (torchrun, one process per GPU): rank r encodes z-slab r of a
@@ -217,7 +217,7 @@ def main():
         ref = d_img.cpu().numpy().view(np.uint16)
         line["decode"] = {"ms": round(dms, 1), "Mpixel_per_s": round(px_rank / dms / 1e3, 1),
                           "exact": bool(np.array_equal(img.reshape(ref.shape), ref)),
-                          "path": "host libbz2 on %d threads + GPU inverse predictor" % threads}
+                          "path": "GPU bzip2 decode + GPU inverse predictor (host libbz2 only for flagged streams, %d threads)" % threads}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)
     if rank == 0:

@@ -71,6 +71,7 @@ struct Dec {
     uint32_t* flags;
     uint32_t* out_len;
     uint32_t* minlen;         // kMaxGroups per stream (min code length)
+    uint32_t sel_cap;         // selectors that fit the decoder's LDS
 };
 
 // MSB-first bit reader over the payload: a 64-bit window of two big-endian
@@ -182,9 +183,10 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
     __shared__ uint16_t sperm[kMaxGroups][kMaxAlpha];
     __shared__ uint8_t slen[kMaxAlpha];
     __shared__ int scnt[kMaxLen + 2], sstart[kMaxLen + 2];
-    // selectors in LDS: a uniform global load of what lane 0 just stored could
-    // be served by the (incoherent) scalar cache
-    __shared__ uint8_t sel[kMaxSel];
+    // selectors in LDS (dynamic: sized for the batch's largest block level; a
+    // uniform global load of what lane 0 just stored could be served by the
+    // incoherent scalar cache)
+    extern __shared__ uint8_t sel[];
     const uint32_t lane = threadIdx.x;
     const uint32_t s = blockIdx.x;
     uint32_t flag = 0;
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         const int alphaSize = (int)nInUse + 2;
         const int nGroups = (int)br.get(3);
         const uint32_t nSel = br.get(15);
-        if (nGroups < 2 || nGroups > kMaxGroups || nSel < 1 || nSel > kMaxSel) { flag = kHost; break; }
+        if (nGroups < 2 || nGroups > kMaxGroups || nSel < 1 || nSel > D.sel_cap) { flag = kHost; break; }
         {  // selectors: unary MTF values, then the inverse MTF
             uint32_t pos = 0x543210u;
             for (uint32_t i = 0; i < nSel && !flag; ++i) {
@@ -297,32 +299,35 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         uint32_t mtfw = (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
         const uint32_t EOB = nInUse + 1;
         int groupNo = -1, groupPos = 0, t = 0;
-        uint32_t next_t = sel[0];
+        // LDS reads of wave-uniform values go through readfirstlane so that the
+        // decode's control flow stays scalar
+        auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+        uint32_t next_t = U(sel[0]);
         auto next_sym = [&]() -> int {
             if (groupPos == 0) {
                 ++groupNo;
                 if ((uint32_t)groupNo >= nSel) return -1;
                 groupPos = 50;
                 t = (int)next_t;
-                next_t = (uint32_t)groupNo + 1 < nSel ? sel[groupNo + 1] : 0u;  // one group ahead
+                next_t = (uint32_t)groupNo + 1 < nSel ? U(sel[groupNo + 1]) : 0u;  // one group ahead
             }
             --groupPos;
-            const uint32_t e = lut[(t << kLutBits) + br.peek(kLutBits)];
+            const uint32_t e = U(lut[(t << kLutBits) + br.peek(kLutBits)]);
             if (e) {
                 br.skip(e >> 9);
                 return (int)(e & 511u) - 1;
             }
             int zn = kLutBits + 1;  // longer than kLutBits: bzip2's limit walk
             int32_t zvec = (int32_t)br.peek(zn);
-            while (zn <= kMaxLen && zvec > slimit[t][zn]) {
+            while (zn <= kMaxLen && zvec > (int32_t)U((uint32_t)slimit[t][zn])) {
                 ++zn;
                 zvec = (int32_t)br.peek(zn);
             }
             if (zn > kMaxLen) return -1;
             br.skip(zn);
-            const int idx = zvec - sbase[t][zn];
+            const int idx = zvec - (int32_t)U((uint32_t)sbase[t][zn]);
             if (idx < 0 || idx >= alphaSize) return -1;
-            return sperm[t][idx];
+            return (int)U(sperm[t][idx]);
         };
         const uint32_t cap = D.cap;
         int sym = next_sym();
@@ -348,8 +353,8 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             const uint32_t nn = (uint32_t)sym - 1;
             const uint32_t v = lane_byte(mtfw, nn);
             // move to front: entries 0 .. nn shift up by one, v goes to 0
-            uint32_t up = __shfl_up(mtfw, 1);
-            if (lane == 0) up = v << 24;
+            // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
+            const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
             const uint32_t sh = (mtfw << 8) | (up >> 24);
             const int k = min(4, max(0, (int)nn - 4 * (int)lane + 1));  // entries of this lane at <= nn
             const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
@@ -515,8 +520,19 @@ __global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
 }
 
 // -------------------------------------------------------------------- RLE1 --
+// One lane per stream (the run state is sequential): the RLE1 text is read 16
+// bytes at a time, output bytes are gathered into words and the CRC advances
+// a word at a time (slicing by 4, tables in LDS).
 __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
 {
+    __shared__ uint32_t T4[4][256];
+    for (uint32_t i = threadIdx.x; i < 1024; i += 64) {
+        const uint32_t k = i >> 8, v = i & 255u;
+        uint32_t c = v << (8 * k);
+        for (int r = 0; r < 4; ++r) c = (c << 8) ^ c_dcrc[c >> 24];
+        T4[k][v] = c;
+    }
+    __syncthreads();
     const uint32_t s = blockIdx.x * 64 + threadIdx.x;
     if (s >= D.count) return;
     if (D.flags[s]) {
@@ -524,35 +540,47 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
         return;
     }
     const uint32_t n = D.n[s];
-    const uint8_t* rle = D.rle + (size_t)s * D.cap;
+    const uint8_t* rle = D.rle + (size_t)s * D.cap;  // cap is a multiple of 256: 16-byte loads stay inside
     uint8_t* out = D.out + (size_t)s * D.out_stride;
     const uint32_t cap = D.out_stride;
     uint32_t o = 0, crc = 0xffffffffu, prev = 256, cnt = 0;
-    bool bad = false;
+    uint32_t acc = 0, na = 0;  // output bytes not yet in the CRC (big endian in acc)
     auto put = [&](uint32_t b) {
         if (o < cap) out[o] = (uint8_t)b;
         ++o;
-        crc = (crc << 8) ^ c_dcrc[(crc >> 24) ^ b];
-    };
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t b = rle[i];
-        if (cnt == 4) {  // the count byte after 4 equal bytes
-            for (uint32_t k = 0; k < b; ++k) put(prev);
-            cnt = 0;
-            prev = 256;
-            continue;
+        acc = (acc << 8) | b;
+        if (++na == 4) {
+            const uint32_t x = crc ^ acc;
+            crc = T4[3][x >> 24] ^ T4[2][(x >> 16) & 255u] ^ T4[1][(x >> 8) & 255u] ^ T4[0][x & 255u];
+            na = 0;
+            acc = 0;
         }
-        put(b);
-        if (b == prev) ++cnt;
-        else {
-            prev = b;
-            cnt = 1;
+    };
+    for (uint32_t i0 = 0; i0 < n; i0 += 16) {
+        const uint4 v4 = *(const uint4*)(rle + i0);
+        const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+        const uint32_t m = min(16u, n - i0);
+        for (uint32_t q = 0; q < m; ++q) {
+            const uint32_t b = (w[q >> 2] >> (8 * (q & 3))) & 255u;
+            if (cnt == 4) {  // the count byte after 4 equal bytes
+                for (uint32_t k = 0; k < b; ++k) put(prev);
+                cnt = 0;
+                prev = 256;
+                continue;
+            }
+            put(b);
+            if (b == prev) ++cnt;
+            else {
+                prev = b;
+                cnt = 1;
+            }
         }
     }
-    if (o > cap) bad = true;
+    for (uint32_t k = 0; k < na; ++k)  // bytes left over: one at a time
+        crc = (crc << 8) ^ c_dcrc[(crc >> 24) ^ ((acc >> (8 * (na - 1 - k))) & 255u)];
     crc = ~crc;
     D.out_len[s] = o;
-    if (bad) D.flags[s] = kHost;
+    if (o > cap) D.flags[s] = kHost;
     else if (crc != D.crc[s]) D.flags[s] = kCrcFail;
 }
 
@@ -653,7 +681,8 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     if (hipMemcpyAsync(d_offs, h_offs, ((size_t)count + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
     const uint32_t g64 = (count + 63) / 64;
-    hipLaunchKernelGGL(bzd_huff, dim3(count), dim3(64), 0, st, D);
+    D.sel_cap = std::min<uint32_t>(kMaxSel, (D.cap + 49) / 50 + 64);
+    hipLaunchKernelGGL(bzd_huff, dim3(count), dim3(64), (D.sel_cap + 15) & ~15u, st, D);
     hipLaunchKernelGGL(bzd_tt, dim3(count), dim3(kTtThreads), 0, st, D);
     hipLaunchKernelGGL(bzd_walk, dim3(count), dim3(kTtThreads), 0, st, D);
     hipLaunchKernelGGL(bzd_rle1, dim3(g64), dim3(64), 0, st, D);

@@ -39,7 +39,7 @@ EXPORTS = [
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
-    "lfm_hip_bzip2_blocks",
+    "lfm_hip_bzip2_blocks", "lfm_hip_bunzip2_workspace_bytes", "lfm_hip_bunzip2_blocks", "lfm_hip_scatter_blocks",
 ]
 
 
@@ -112,6 +112,12 @@ def lib():
     L.lfm_hip_bzip2_blocks.argtypes = [vp, u32p, u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.c_uint32, vp, ctypes.c_size_t, vp,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32), vp]
+    L.lfm_hip_bunzip2_workspace_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.lfm_hip_bunzip2_workspace_bytes.restype = ctypes.c_size_t
+    L.lfm_hip_bunzip2_blocks.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, vp, ctypes.c_uint32,
+                                         vp, ctypes.c_size_t, u32p, u32p, vp]
+    L.lfm_hip_scatter_blocks.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p,
+                                         ctypes.c_uint32, vp, vp]
     L.lfm_hip_select_workspace_bytes.restype = ctypes.c_size_t
     L.lfm_hip_select_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     L.lfm_hip_select.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p,
@@ -402,6 +408,28 @@ def bzip2_device(d_img, dims, block, bpp, level=None, first=0, count=None, strea
             out.append(host[o:o + sizes[i]])
             o += sizes[i]
     return out, list(flags)
+
+
+def bunzip2_device(streams, out_stride, device="cuda", stream=None):
+    """GPU bzip2 decode of single-block streams (bytes objects).  Returns
+    ([bytes per stream, or None where the device flagged it for the host
+    library], flags): flag 1 = host library, 2 = block CRC mismatch."""
+    count = len(streams)
+    offs = np.zeros(count + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in streams])
+    blob = b"".join(streams) + bytes(64)
+    d_pay = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device)
+    ws_bytes = lib().lfm_hip_bunzip2_workspace_bytes(count, out_stride)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+    out = torch.empty(count * out_stride, dtype=torch.uint8, device=device)
+    lens = (ctypes.c_uint32 * count)()
+    flags = (ctypes.c_uint32 * count)()
+    _check(lib().lfm_hip_bunzip2_blocks(d_pay.data_ptr(), offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), count,
+                                        out.data_ptr(), out_stride, ws.data_ptr(), ws_bytes, lens, flags,
+                                        _stream(stream)), "lfm_hip_bunzip2_blocks")
+    host = out.cpu().numpy()
+    res = [None if flags[i] else host[i * out_stride:i * out_stride + lens[i]].tobytes() for i in range(count)]
+    return res, list(flags)
 
 
 def synth_device(d_out, X, Y, Z, T, t_index=0, idx0=0, seed=0x4C464D00, stream=None):

@@ -415,3 +415,37 @@ def test_decode_roundtrip_through_gpu(lfmlib, oracle, gpu, tmp_path):
         finally:
             lfmlib.set_family("tiles")
         assert np.array_equal(out, img), fam
+
+
+@pytest.mark.gpu
+def test_gpu_bunzip2_matches_libbz2(lfmlib, gpu):
+    """GPU bzip2 decoder against the system libbz2 (Python's bz2,
+    the same format as the reference's vendored 1.0.6): streams of every level,
+    long runs (RLE1 count bytes, RUNA/RUNB), random and periodic data, tiny
+    blocks; a two-block stream and a damaged stream are flagged for the host."""
+    import bz2
+    rng = np.random.default_rng(7)
+    cases = []
+    for level in (1, 2, 5, 9):
+        cases.append((rng.integers(0, 256, 90000, dtype=np.uint8).tobytes(), level))
+    cases += [
+        (bytes(150000), 2),                                        # one long run
+        (b"\x07" * 5 + b"ab" * 300 + b"\x00" * 1000, 1),          # runs of 4+, periodic
+        (rng.integers(0, 4, 140000, dtype=np.uint8).tobytes(), 2),  # small alphabet
+        ((np.arange(147456) % 251).astype(np.uint8).tobytes(), 2),
+        (b"x", 1),
+        (b"hello, light field", 9),
+        (rng.integers(0, 2, 150000, dtype=np.uint8).repeat(3)[:147456].tobytes(), 2),
+    ]
+    streams = [bz2.compress(d, lv) for d, lv in cases]
+    out, flags = lfmlib.bunzip2_device(streams, 160000)
+    for (d, lv), o, f in zip(cases, out, flags):
+        assert f == 0, (lv, len(d), f)
+        assert o == d, (lv, len(d))
+    # two bzip2 blocks (more than 100k after RLE1 at level 1) -> host; a flipped bit -> not accepted
+    big = rng.integers(0, 256, 150000, dtype=np.uint8).tobytes()
+    bad = bytearray(bz2.compress(b"some data to damage" * 100, 1))
+    bad[len(bad) // 2] ^= 0x10
+    out, flags = lfmlib.bunzip2_device([bz2.compress(big, 1), bytes(bad)], 160000)
+    assert flags[0] == 1 and out[0] is None
+    assert flags[1] != 0 and out[1] is None
