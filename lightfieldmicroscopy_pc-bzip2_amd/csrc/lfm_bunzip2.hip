@@ -127,38 +127,43 @@ struct BitReader {
 //  * a RUNA/RUNB run is written by all 64 lanes.
 // Output: the BWT last column ll[], n, origPtr, the block CRC.
 struct WaveBits {
-    const uint32_t* w;
-    uint64_t pos, wpos, end;
-    uint64_t win;
-    uint32_t q0, q1, q2, q3;  // words wpos + 2 .. wpos + 5
-    __device__ __forceinline__ uint32_t word(uint64_t i) const { return __builtin_bswap32(w[i]); }
+    const uint32_t* w;   // the stream's first (aligned) payload word
+    uint32_t wi;         // next word to enter the queue
+    uint64_t win;        // 64 bits from the current word on
+    uint32_t off;        // bits of win already consumed (< 32)
+    uint32_t used;       // bits consumed since the stream start
+    uint32_t total;      // bits in the stream
+    uint32_t q0, q1, q2, q3;
+    __device__ __forceinline__ uint32_t word(uint32_t i) const { return __builtin_bswap32(w[i]); }
     __device__ __forceinline__ void init(const uint8_t* payload, uint64_t byte0, uint64_t byte1)
     {
-        w = (const uint32_t*)payload;
-        pos = byte0 * 8;
-        end = byte1 * 8;
-        wpos = pos >> 5;
-        win = ((uint64_t)word(wpos) << 32) | word(wpos + 1);
-        q0 = word(wpos + 2);
-        q1 = word(wpos + 3);
-        q2 = word(wpos + 4);
-        q3 = word(wpos + 5);
+        w = (const uint32_t*)payload + (byte0 >> 2);
+        off = (uint32_t)(byte0 & 3) * 8;
+        used = 0;
+        total = (uint32_t)(byte1 - byte0) * 8;
+        win = ((uint64_t)word(0) << 32) | word(1);
+        q0 = word(2);
+        q1 = word(3);
+        q2 = word(4);
+        q3 = word(5);
+        wi = 6;
     }
-    __device__ __forceinline__ uint32_t peek(uint32_t nb) const
+    __device__ __forceinline__ uint32_t peek(uint32_t nb) const  // nb in 1..32
     {
-        const uint32_t off = (uint32_t)(pos - 32 * wpos);
         return (uint32_t)((win << off) >> (64 - nb));
     }
-    __device__ __forceinline__ void skip(uint32_t nb)
+    __device__ __forceinline__ void skip(uint32_t nb)  // nb <= 32
     {
-        pos += nb;
-        while (pos - 32 * wpos >= 32) {
-            ++wpos;
+        off += nb;
+        used += nb;
+        if (off >= 32) {
+            off -= 32;
             win = (win << 32) | q0;
             q0 = q1;
             q1 = q2;
             q2 = q3;
-            q3 = pos < end + 64 ? word(wpos + 5) : 0u;  // never past the payload's slack
+            q3 = used < total + 256 ? word(wi) : 0u;  // never past the payload's slack
+            ++wi;
         }
     }
     __device__ __forceinline__ uint32_t get(uint32_t nb)
@@ -167,7 +172,7 @@ struct WaveBits {
         skip(nb);
         return v;
     }
-    __device__ __forceinline__ bool over() const { return pos > end; }
+    __device__ __forceinline__ bool over() const { return used > total; }
 };
 
 __device__ __forceinline__ uint32_t lane_byte(uint32_t w4, uint32_t idx)  // entry idx of a 4-per-lane list
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         auto next_sym = [&]() -> int {
             if (groupPos == 0) {
                 ++groupNo;
-                if ((uint32_t)groupNo >= nSel) return -1;
+                if ((uint32_t)groupNo >= nSel || br.over()) return -1;
                 groupPos = 50;
                 t = (int)next_t;
                 next_t = (uint32_t)groupNo + 1 < nSel ? U(sel[groupNo + 1]) : 0u;  // one group ahead
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         const uint32_t cap = D.cap;
         int sym = next_sym();
         while (true) {
-            if (sym < 0 || br.over()) { flag = kHost; break; }
+            if (sym < 0) { flag = kHost; break; }
             if ((uint32_t)sym == EOB) break;
             if (sym <= 1) {  // RUNA / RUNB: a run of the list front
                 uint32_t es = 0, N = 1;
