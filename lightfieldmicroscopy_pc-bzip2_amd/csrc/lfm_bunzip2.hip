@@ -56,11 +56,6 @@ struct Dec {
     uint8_t* ll;              // cap per stream
     uint32_t* tt;             // cap per stream
     uint8_t* rle;             // cap per stream
-    uint16_t* lut;            // kMaxGroups << kLutBits per stream
-    int32_t* limit;           // kMaxGroups * (kMaxLen + 2) per stream
-    int32_t* base;            // kMaxGroups * (kMaxLen + 2) per stream
-    uint16_t* perm;           // kMaxGroups * kMaxAlpha per stream
-    uint8_t* sel;             // kMaxSel per stream
     uint32_t mcap;            // markers per stream
     uint32_t* mnext;
     uint32_t* mlen;
@@ -70,7 +65,6 @@ struct Dec {
     uint32_t* crc;
     uint32_t* flags;
     uint32_t* out_len;
-    uint32_t* minlen;         // kMaxGroups per stream (min code length)
     uint32_t sel_cap;         // selectors that fit the decoder's LDS
 };
 
@@ -621,13 +615,8 @@ extern "C" size_t lfm_hip_bunzip2_workspace_bytes(uint32_t count, uint32_t out_s
     b += al((size_t)count * cap);          // ll
     b += al((size_t)count * cap * 4);      // tt
     b += al((size_t)count * cap);          // rle
-    b += al((size_t)count * (kMaxGroups << kLutBits) * 2);
-    b += 2 * al((size_t)count * kMaxGroups * (kMaxLen + 2) * 4);
-    b += al((size_t)count * kMaxGroups * kMaxAlpha * 2);
-    b += al((size_t)count * kMaxSel);
     b += 3 * al((size_t)count * mc * 4);
     b += 6 * al((size_t)count * 4 + 64);
-    b += al((size_t)count * kMaxGroups * 4);
     return b;
 }
 
@@ -671,18 +660,12 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     D.ll = take((size_t)count * D.cap);
     D.tt = (uint32_t*)take((size_t)count * D.cap * 4);
     D.rle = take((size_t)count * D.cap);
-    D.lut = (uint16_t*)take((size_t)count * (kMaxGroups << kLutBits) * 2);
-    D.limit = (int32_t*)take((size_t)count * kMaxGroups * (kMaxLen + 2) * 4);
-    D.base = (int32_t*)take((size_t)count * kMaxGroups * (kMaxLen + 2) * 4);
-    D.perm = (uint16_t*)take((size_t)count * kMaxGroups * kMaxAlpha * 2);
-    D.sel = take((size_t)count * kMaxSel);
     D.mnext = (uint32_t*)take((size_t)count * D.mcap * 4);
     D.mlen = (uint32_t*)take((size_t)count * D.mcap * 4);
     D.mstart = (uint32_t*)take((size_t)count * D.mcap * 4);
     uint32_t** small[] = {&D.n, &D.orig, &D.crc, &D.flags, &D.out_len};
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
     (void)take((size_t)count * 4 + 64);
-    D.minlen = (uint32_t*)take((size_t)count * kMaxGroups * 4);
     if (hipMemcpyAsync(d_offs, h_offs, ((size_t)count + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
     const uint32_t g64 = (count + 63) / 64;
