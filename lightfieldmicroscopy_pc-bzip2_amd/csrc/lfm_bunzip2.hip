@@ -5,12 +5,12 @@
 // (klb_imageIO.cpp:1748-1821 via BZ2_bzBuffToBuffDecompress); here a batch of
 // streams is decoded on the device, restating bzip2-1.0.6's decompress.c:
 //
-//   bzd_huff    one lane per stream: stream / block headers, the mapping
+//   bzd_huff    one wave per stream: stream / block headers, the mapping
 //               table, selectors (unary MTF), delta-coded code lengths, the
-//               decode tables (a 10-bit lookup table per Huffman table plus
+//               decode tables (an 8-bit lookup table per Huffman table plus
 //               limit / base / perm for longer codes, BZ2_hbCreateDecodeTables),
 //               then the symbols: RUNA/RUNB runs and move-to-front (the list
-//               of each lane in LDS, interleaved), giving the BWT last column
+//               in registers, 4 entries per lane), giving the BWT last column
 //               ll[] and the block length n.  Anything else (several blocks,
 //               randomised blocks, a malformed stream) is flagged for the host.
 //   bzd_tt      one workgroup per stream: byte counts, then LF(i) = C[ll[i]] +
@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "lfm_hip.h"
@@ -111,36 +112,62 @@ struct BitReader {
 // One wave per stream.  The decode is one sequential chain per stream, so
 // every lane runs the same (wave-uniform) header and symbol code; what the
 // wave buys is storage and wide steps:
-//  * the decode tables live in LDS (a 10-bit lookup table per Huffman table:
-//    one broadcast LDS read decodes most symbols);
-//  * the move-to-front list and seqToUnseq are registers, 4 entries per lane:
-//    a move-to-front of position m is one lane shift and a byte select, not m
-//    serial moves; list[m] is one readlane;
-//  * the bit window is refilled from a 4-word lookahead queue, so the load of
-//    a payload word is issued ~4 refills before it is needed;
-//  * a RUNA/RUNB run is written by all 64 lanes.
+//  * the decode tables live in LDS (an LB-bit lookup table per Huffman table:
+//    one broadcast LDS read decodes most symbols; longer codes walk bzip2's
+//    limit table).  The LDS per stream is kept near 10 KB so that a whole
+//    batch (~16 streams per CU) is resident at once: the decode is latency
+//    bound per wave, so resident waves are throughput;
+//  * the move-to-front list holds the output bytes themselves (seqToUnseq
+//    applied up front), 4 entries per lane: a move-to-front of position m is
+//    one lane shift and a byte select, not m serial moves; list[m] is one
+//    readlane;
+//  * the bit window is refilled from a vector window: lane l holds payload
+//    word base + l and a second register the next 64 words, loaded 64 words
+//    (~300 symbols) before they are needed; a refill is one readlane (a
+//    scalar-register queue made the compiler wait for every refill load right
+//    where it was issued);
+//  * output bytes collect in a register (one byte per lane) and leave in
+//    64-byte stores; a RUNA/RUNB run fills lanes of it, long runs are written
+//    by all 64 lanes;
+//  * one flat loop per symbol (one bit-window advance, run digits accumulate
+//    until the next non-run symbol), so the per-symbol code stays short.
 // Output: the BWT last column ll[], n, origPtr, the block CRC.
 struct WaveBits {
     const uint32_t* w;   // the stream's first (aligned) payload word
-    uint32_t wi;         // next word to enter the queue
+    uint32_t nw;         // words that start inside the stream (later ones read as 0)
+    uint32_t base;       // word held by lane 0 of vq
+    uint32_t vq, vn;     // per lane: word base + lane (byte-swapped), base + 64 + lane (raw)
+    uint32_t wi;         // next word to enter the bit window
     uint64_t win;        // 64 bits from the current word on
     uint32_t off;        // bits of win already consumed (< 32)
     uint32_t used;       // bits consumed since the stream start
     uint32_t total;      // bits in the stream
-    uint32_t q0, q1, q2, q3;
-    __device__ __forceinline__ uint32_t word(uint32_t i) const { return __builtin_bswap32(w[i]); }
+    // raw (unswapped) load with a clamped index: no branch and no use of the
+    // value next to the load, so the wait lands where the word is first needed
+    __device__ __forceinline__ uint32_t raw(uint32_t i) const { return w[min(i, nw - 1)]; }
+    __device__ __forceinline__ uint32_t fix(uint32_t v, uint32_t i) const { return i < nw ? __builtin_bswap32(v) : 0u; }
+    __device__ __forceinline__ uint32_t next()
+    {
+        if (wi - base == 64) {
+            base += 64;
+            vq = fix(vn, base + threadIdx.x);
+            vn = raw(base + 64 + threadIdx.x);
+        }
+        return (uint32_t)__builtin_amdgcn_readlane((int)vq, (int)(wi++ - base));
+    }
     __device__ __forceinline__ void init(const uint8_t* payload, uint64_t byte0, uint64_t byte1)
     {
         w = (const uint32_t*)payload + (byte0 >> 2);
+        nw = (uint32_t)((byte1 - (byte0 & ~3ull) + 3) >> 2);
         off = (uint32_t)(byte0 & 3) * 8;
         used = 0;
         total = (uint32_t)(byte1 - byte0) * 8;
-        win = ((uint64_t)word(0) << 32) | word(1);
-        q0 = word(2);
-        q1 = word(3);
-        q2 = word(4);
-        q3 = word(5);
-        wi = 6;
+        base = 0;
+        vq = fix(raw(threadIdx.x), threadIdx.x);
+        vn = raw(64 + threadIdx.x);
+        wi = 2;
+        win = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vq, 0) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)vq, 1);
     }
     __device__ __forceinline__ uint32_t peek(uint32_t nb) const  // nb in 1..32
     {
@@ -152,12 +179,7 @@ struct WaveBits {
         used += nb;
         if (off >= 32) {
             off -= 32;
-            win = (win << 32) | q0;
-            q0 = q1;
-            q1 = q2;
-            q2 = q3;
-            q3 = used < total + 256 ? word(wi) : 0u;  // never past the payload's slack
-            ++wi;
+            win = (win << 32) | next();
         }
     }
     __device__ __forceinline__ uint32_t get(uint32_t nb)
@@ -169,23 +191,19 @@ struct WaveBits {
     __device__ __forceinline__ bool over() const { return used > total; }
 };
 
-__device__ __forceinline__ uint32_t lane_byte(uint32_t w4, uint32_t idx)  // entry idx of a 4-per-lane list
-{
-    return (__builtin_amdgcn_readlane(w4, idx >> 2) >> (8 * (idx & 3))) & 0xFFu;
-}
-
+template <int LB>
 __global__ __launch_bounds__(64) void bzd_huff(Dec D)
 {
-    __shared__ uint16_t lut[kMaxGroups << kLutBits];
+    __shared__ uint16_t lut[kMaxGroups << LB];
     __shared__ int32_t slimit[kMaxGroups][kMaxLen + 2];
     __shared__ int32_t sbase[kMaxGroups][kMaxLen + 2];
     __shared__ uint16_t sperm[kMaxGroups][kMaxAlpha];
     __shared__ uint8_t slen[kMaxAlpha];
     __shared__ int scnt[kMaxLen + 2], sstart[kMaxLen + 2];
-    // selectors in LDS (dynamic: sized for the batch's largest block level; a
-    // uniform global load of what lane 0 just stored could be served by the
-    // incoherent scalar cache)
-    extern __shared__ uint8_t sel[];
+    // selectors in LDS, 8 per word (dynamic: sized for the batch's largest
+    // block level; a uniform global load of what lane 0 just stored could be
+    // served by the incoherent scalar cache)
+    extern __shared__ uint32_t sel[];
     const uint32_t lane = threadIdx.x;
     const uint32_t s = blockIdx.x;
     uint32_t flag = 0;
@@ -195,6 +213,9 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
     uint8_t* ll = D.ll + (size_t)s * D.cap;
     uint32_t nblock = 0, origPtr = 0, bcrc = 0;
     uint32_t s2u = 0;  // seqToUnseq, entries 4 * lane .. 4 * lane + 3
+    // LDS reads of wave-uniform values go through readfirstlane so that the
+    // decode's control flow stays scalar
+    auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
     do {
         if (b1 - b0 < 14) { flag = kHost; break; }
         if (br.get(24) != 0x425A68u) { flag = kHost; break; }  // "BZh"
@@ -223,7 +244,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         const uint32_t nSel = br.get(15);
         if (nGroups < 2 || nGroups > kMaxGroups || nSel < 1 || nSel > D.sel_cap) { flag = kHost; break; }
         {  // selectors: unary MTF values, then the inverse MTF
-            uint32_t pos = 0x543210u;
+            uint32_t pos = 0x543210u, word = 0;
             for (uint32_t i = 0; i < nSel && !flag; ++i) {
                 uint32_t j = 0;
                 while (br.get(1)) {
@@ -232,7 +253,11 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                 const uint32_t v = (pos >> (4 * j)) & 15u;
                 const uint32_t m = (1u << (4 * (j + 1))) - 1u;
                 pos = (pos & ~m) | (((pos << 4) | v) & m);
-                if (lane == 0) sel[i] = (uint8_t)v;
+                word |= v << (4 * (i & 7));
+                if ((i & 7) == 7 || i + 1 == nSel) {
+                    if (lane == 0) sel[i >> 3] = word;
+                    word = 0;
+                }
             }
             if (flag) break;
         }
@@ -279,11 +304,11 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             }
             __syncthreads();
             // lookup table: entry = sym + 1 (0: longer code) | length << 9
-            uint16_t* lt = lut + (t << kLutBits);
-            for (int e = lane; e < (1 << kLutBits); e += 64) {
+            uint16_t* lt = lut + (t << LB);
+            for (int e = lane; e < (1 << LB); e += 64) {
                 uint16_t ent = 0;
-                for (int l = mn; l <= min(mx, kLutBits); ++l) {
-                    const int c = e >> (kLutBits - l);  // the first l bits of e
+                for (int l = mn; l <= min(mx, LB); ++l) {
+                    const int c = e >> (LB - l);  // the first l bits of e
                     if (c <= slimit[t][l] && c > slimit[t][l] - scnt[l]) {
                         ent = (uint16_t)((sperm[t][c - sbase[t][l]] + 1) | (l << 9));
                         break;
@@ -295,74 +320,88 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         }
         if (flag) break;
         // symbols
-        uint32_t mtfw = (4 * lane) | ((4 * lane + 1) << 8) | ((4 * lane + 2) << 16) | ((4 * lane + 3) << 24);
+        uint32_t mtfw = s2u;   // the move-to-front list, as output bytes
+        uint32_t obuf = 0;     // pending output bytes, byte i of the batch in lane i
+        uint32_t op = 0;       // pending bytes (they belong at ll[nblock - op ..])
         const uint32_t EOB = nInUse + 1;
-        int groupNo = -1, groupPos = 0, t = 0;
-        // LDS reads of wave-uniform values go through readfirstlane so that the
-        // decode's control flow stays scalar
-        auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
-        uint32_t next_t = U(sel[0]);
-        auto next_sym = [&]() -> int {
-            if (groupPos == 0) {
-                ++groupNo;
-                if ((uint32_t)groupNo >= nSel || br.over()) return -1;
-                groupPos = 50;
-                t = (int)next_t;
-                next_t = (uint32_t)groupNo + 1 < nSel ? U(sel[groupNo + 1]) : 0u;  // one group ahead
-            }
-            --groupPos;
-            const uint32_t e = U(lut[(t << kLutBits) + br.peek(kLutBits)]);
-            if (e) {
-                br.skip(e >> 9);
-                return (int)(e & 511u) - 1;
-            }
-            int zn = kLutBits + 1;  // longer than kLutBits: bzip2's limit walk
-            int32_t zvec = (int32_t)br.peek(zn);
-            while (zn <= kMaxLen && zvec > (int32_t)U((uint32_t)slimit[t][zn])) {
-                ++zn;
-                zvec = (int32_t)br.peek(zn);
-            }
-            if (zn > kMaxLen) return -1;
-            br.skip(zn);
-            const int idx = zvec - (int32_t)U((uint32_t)sbase[t][zn]);
-            if (idx < 0 || idx >= alphaSize) return -1;
-            return (int)U(sperm[t][idx]);
-        };
         const uint32_t cap = D.cap;
-        int sym = next_sym();
+        uint32_t g = 0, gleft = 0, tb = 0, selw = 0;
+        uint32_t es = 0, rs = 0;  // pending RUNA/RUNB run: length, next digit
+        const int kk0 = 1 - 4 * (int)lane;
         while (true) {
-            if (sym < 0) { flag = kHost; break; }
-            if ((uint32_t)sym == EOB) break;
-            if (sym <= 1) {  // RUNA / RUNB: a run of the list front
-                uint32_t es = 0, N = 1;
-                do {
-                    es += (uint32_t)(sym + 1) * N;
-                    N <<= 1;
-                    if (N > (1u << 21)) { flag = kHost; break; }
-                    sym = next_sym();
-                } while (sym >= 0 && sym <= 1);
-                if (flag) break;
-                if (nblock + es > cap) { flag = kHost; break; }
-                const uint8_t uc = (uint8_t)lane_byte(s2u, lane_byte(mtfw, 0));
-                for (uint32_t k = lane; k < es; k += 64) ll[nblock + k] = uc;
-                nblock += es;
-                continue;  // sym already holds the next symbol
+            if (gleft == 0) {  // next group of 50 symbols: its table
+                if (g >= nSel || br.over()) { flag = kHost; break; }
+                if ((g & 7) == 0) selw = U(sel[g >> 3]);
+                tb = ((selw >> (4 * (g & 7))) & 15u) << LB;
+                ++g;
+                gleft = 50;
             }
+            --gleft;
+            const uint32_t e = U(lut[tb + br.peek(LB)]);
+            uint32_t len = e >> 9, sym = (e & 511u) - 1u;
+            if (e == 0) {  // longer than LB bits: bzip2's limit walk
+                const uint32_t t = tb >> LB;
+                uint32_t zn = LB + 1;
+                int32_t zvec = (int32_t)br.peek(zn);
+                while (zn <= kMaxLen && zvec > (int32_t)U((uint32_t)slimit[t][zn])) {
+                    ++zn;
+                    zvec = (int32_t)br.peek(zn);
+                }
+                if (zn > kMaxLen) { flag = kHost; break; }
+                const int idx = zvec - (int32_t)U((uint32_t)sbase[t][zn]);
+                if (idx < 0 || idx >= alphaSize) { flag = kHost; break; }
+                sym = U(sperm[t][idx]);
+                len = zn;
+            }
+            br.skip(len);
+            if (sym <= 1) {  // RUNA / RUNB: one digit of a run of the list front
+                es += (sym + 1) << rs;
+                if (++rs > 21) { flag = kHost; break; }
+                continue;
+            }
+            if (rs) {  // the run ends: es copies of the list front
+                if (nblock + es > cap) { flag = kHost; break; }
+                const uint32_t uc = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
+                nblock += es;
+                while (es) {
+                    if (op == 0 && es >= 64) {  // whole 64-byte pieces straight out
+                        const uint32_t whole = es & ~63u;
+                        const uint32_t at = nblock - es;
+                        for (uint32_t k = lane; k < whole; k += 64) ll[at + k] = (uint8_t)uc;
+                        es -= whole;
+                        continue;
+                    }
+                    const uint32_t take = min(es, 64u - op);
+                    obuf = lane - op < take ? uc : obuf;
+                    op += take;
+                    es -= take;
+                    if (op == 64) {
+                        ll[nblock - es - 64 + lane] = (uint8_t)obuf;
+                        op = 0;
+                    }
+                }
+                rs = 0;
+            }
+            if (sym == EOB) break;
             if (nblock >= cap) { flag = kHost; break; }
-            const uint32_t nn = (uint32_t)sym - 1;
-            const uint32_t v = lane_byte(mtfw, nn);
+            const uint32_t nn = sym - 1;
+            const uint32_t v = ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)(nn >> 2)) >> (8 * (nn & 3))) & 0xFFu;
             // move to front: entries 0 .. nn shift up by one, v goes to 0
             // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
             const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
             const uint32_t sh = (mtfw << 8) | (up >> 24);
-            const int k = min(4, max(0, (int)nn - 4 * (int)lane + 1));  // entries of this lane at <= nn
+            const int k = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
             const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
             mtfw = (sh & msk) | (mtfw & ~msk);
-            if (lane == 0) ll[nblock] = (uint8_t)lane_byte(s2u, v);
+            obuf = lane == op ? v : obuf;
             ++nblock;
-            sym = next_sym();
+            if (++op == 64) {
+                ll[nblock - 64 + lane] = (uint8_t)obuf;
+                op = 0;
+            }
         }
         if (flag) break;
+        if (lane < op) ll[nblock - op + lane] = (uint8_t)obuf;
         if (origPtr >= nblock || nblock == 0) { flag = kHost; break; }
         // end of stream: exactly one block
         const uint32_t e1 = br.get(24), e2 = br.get(24);
@@ -670,7 +709,15 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
         return LFM_HIP_ERUNTIME;
     const uint32_t g64 = (count + 63) / 64;
     D.sel_cap = std::min<uint32_t>(kMaxSel, (D.cap + 49) / 50 + 64);
-    hipLaunchKernelGGL(bzd_huff, dim3(count), dim3(64), (D.sel_cap + 15) & ~15u, st, D);
+    const size_t sel_lds = ((D.sel_cap + 7) / 8 * 4 + 15) & ~(size_t)15;
+    static const int lut_bits = [] {
+        const char* e = getenv("LFM_BZD_LUT_BITS");
+        const int b = e ? atoi(e) : 8;
+        return b == 9 || b == 10 ? b : 8;
+    }();
+    if (lut_bits == 10) hipLaunchKernelGGL(bzd_huff<10>, dim3(count), dim3(64), sel_lds, st, D);
+    else if (lut_bits == 9) hipLaunchKernelGGL(bzd_huff<9>, dim3(count), dim3(64), sel_lds, st, D);
+    else hipLaunchKernelGGL(bzd_huff<8>, dim3(count), dim3(64), sel_lds, st, D);
     hipLaunchKernelGGL(bzd_tt, dim3(count), dim3(kTtThreads), 0, st, D);
     hipLaunchKernelGGL(bzd_walk, dim3(count), dim3(kTtThreads), 0, st, D);
     hipLaunchKernelGGL(bzd_rle1, dim3(g64), dim3(64), 0, st, D);

@@ -2107,24 +2107,32 @@ __global__ __launch_bounds__(256) void compact_streams(Batch B, const uint64_t* 
     }
 }
 
-// exclusive offsets of the streams' byte counts (one wave, 64 at a time)
-__global__ __launch_bounds__(64) void scan_offsets(const uint32_t* __restrict__ nbytes, uint32_t n,
-                                                   uint64_t* __restrict__ offs)
+// exclusive offsets of the streams' byte counts: one workgroup, every thread
+// sums a contiguous run, one block scan, then every thread writes its run
+__global__ __launch_bounds__(1024) void scan_offsets(const uint32_t* __restrict__ nbytes, uint32_t n,
+                                                     uint64_t* __restrict__ offs)
 {
-    const uint32_t lane = threadIdx.x;
-    uint64_t carry = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint64_t v = i < n ? nbytes[i] : 0u;
-        uint64_t inc = v;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t o = __shfl_up(inc, d);
-            if ((int)lane >= d) inc += o;
-        }
-        if (i < n) offs[i] = carry + inc - v;
-        carry += __shfl(inc, 63);
+    __shared__ uint64_t wsum64[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t a = min(n, t * per), b = min(n, a + per);
+    uint64_t sum = 0;
+    for (uint32_t i = a; i < b; ++i) sum += nbytes[i];
+    uint64_t inc = sum;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(inc, d);
+        if ((int)lane >= d) inc += o;
     }
-    if (lane == 0) offs[n] = carry;
+    if (lane == 63) wsum64[wave] = inc;
+    __syncthreads();
+    uint64_t acc = inc - sum;
+    for (uint32_t w = 0; w < wave; ++w) acc += wsum64[w];
+    for (uint32_t i = a; i < b; ++i) {
+        offs[i] = acc;
+        acc += nbytes[i];
+    }
+    if (b == n && a < b) offs[n] = acc;
+    if (n == 0 && t == 0) offs[0] = 0;
 }
 
 } // namespace bz
@@ -2512,7 +2520,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
-    hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(64), 0, st, B.out_bytes, count, offs);
+    hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(1024), 0, st, B.out_bytes, count, offs);
     hipLaunchKernelGGL(compact_streams, dim3(count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
     if (!ok()) return LFM_HIP_ERUNTIME;
     std::vector<uint32_t> nbytes(count);
