@@ -21,8 +21,11 @@
 //               walker follows tt from its marker to the next one and counts,
 //               one lane chains the segments to their output offsets, the
 //               walkers walk again and write the RLE1 text.
-//   bzd_rle1    one lane per stream: RLE1 decode (4 equal bytes + a count) into
-//               the output block, CRC-32 of the block checked against the header.
+//   bzd_rle1    one wave per stream: RLE1 decode (4 equal bytes + a count) into
+//               the output block from 64 text segments (their start states
+//               resolved by running every start state), CRC-32 of the block in
+//               64 segments combined by polynomial shifts, checked against the
+//               header.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
@@ -558,68 +561,205 @@ __global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
 }
 
 // -------------------------------------------------------------------- RLE1 --
-// One lane per stream (the run state is sequential): the RLE1 text is read 16
-// bytes at a time, output bytes are gathered into words and the CRC advances
-// a word at a time (slicing by 4, tables in LDS).
+// One wave per stream.  RLE1 decoding is a 5-state machine over the text
+// (state = equal bytes seen, 0 right after a count byte; in state 4 the byte
+// is a count: it repeats the previous byte that many times), so the text is
+// cut into 64 lane segments (16-byte aligned) and decoded in three steps:
+//  A  every lane runs its segment from all five start states at once (the
+//     paths meet after a few bytes in any real stream, then one path runs
+//     alone) and keeps, per start state, the end state and the output length;
+//  B  one uniform pass over the 64 lanes chains them: each lane's start state
+//     and output offset;
+//  C  every lane decodes its segment again, writing its bytes at its offset.
+// The block CRC then runs over the output in 64 equal segments aligned to its
+// end (leading zero bytes do not change a zero-initialised CRC), combined in
+// a 6-level tree: crc(L || R) = crc(L) * x^(8|R|) mod P ^ crc(R).
+__constant__ uint32_t c_xpow[24];  // x^(8 * 2^k) mod P
+
+// a(x) * b(x) mod P, MSB-first CRC-32 polynomials (P = x^32 + 0x04C11DB7)
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+        r = (r << 1) ^ ((r >> 31) ? 0x04C11DB7u : 0u);
+        r ^= ((b >> i) & 1u) ? a : 0u;
+    }
+    return r;
+}
+
+// x^(8 L) mod P: the CRC shift over L zero bytes
+__device__ __forceinline__ uint32_t crc_xpow8(uint32_t L)
+{
+    uint32_t r = 1u;  // x^0
+    for (int k = 0; k < 24 && L; ++k, L >>= 1)
+        if (L & 1u) r = crc_mulmod(r, c_xpow[k]);
+    return r;
+}
+
+constexpr int kRleSeg = 16;  // segment alignment (bytes)
+
+// per-lane sequential reader of the RLE1 text, 16 bytes at a time with the
+// next chunk loaded one chunk ahead
+struct TextChunks {
+    const uint8_t* p;
+    uint32_t cap;
+    __device__ __forceinline__ uint4 load(uint32_t at) const
+    {
+        return at < cap ? *(const uint4*)(p + at) : uint4{0u, 0u, 0u, 0u};
+    }
+};
+
+__device__ __forceinline__ uint32_t chunk_byte(const uint4& q, int j)  // j compile-time after unrolling
+{
+    const uint32_t w = j < 4 ? q.x : j < 8 ? q.y : j < 12 ? q.z : q.w;
+    return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
 __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
 {
-    __shared__ uint32_t T4[4][256];
-    for (uint32_t i = threadIdx.x; i < 1024; i += 64) {
-        const uint32_t k = i >> 8, v = i & 255u;
-        uint32_t c = v << (8 * k);
-        for (int r = 0; r < 4; ++r) c = (c << 8) ^ c_dcrc[c >> 24];
-        T4[k][v] = c;
-    }
-    __syncthreads();
-    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
-    if (s >= D.count) return;
+    __shared__ uint32_t T1[256];
+    __shared__ uint32_t smap[64], scnt[5][64], sst[64], soff[64];
+    __shared__ uint32_t s_total;
+    const uint32_t lane = threadIdx.x, s = blockIdx.x;
+    for (uint32_t i = lane; i < 256; i += 64) T1[i] = c_dcrc[i];
     if (D.flags[s]) {
-        D.out_len[s] = 0;
+        if (lane == 0) D.out_len[s] = 0;
         return;
     }
     const uint32_t n = D.n[s];
-    const uint8_t* rle = D.rle + (size_t)s * D.cap;  // cap is a multiple of 256: 16-byte loads stay inside
+    const uint8_t* rle = D.rle + (size_t)s * D.cap;
     uint8_t* out = D.out + (size_t)s * D.out_stride;
     const uint32_t cap = D.out_stride;
-    uint32_t o = 0, crc = 0xffffffffu, prev = 256, cnt = 0;
-    uint32_t acc = 0, na = 0;  // output bytes not yet in the CRC (big endian in acc)
-    auto put = [&](uint32_t b) {
-        if (o < cap) out[o] = (uint8_t)b;
-        ++o;
-        acc = (acc << 8) | b;
-        if (++na == 4) {
-            const uint32_t x = crc ^ acc;
-            crc = T4[3][x >> 24] ^ T4[2][(x >> 16) & 255u] ^ T4[1][(x >> 8) & 255u] ^ T4[0][x & 255u];
-            na = 0;
-            acc = 0;
+    const TextChunks tx{rle, D.cap};
+    const uint32_t seg = ((n + 63) / 64 + kRleSeg - 1) / kRleSeg * kRleSeg;
+    const uint32_t a = min(n, lane * seg), b = min(n, a + seg);
+    const uint32_t before = a ? (uint32_t)rle[a - 1] : 256u;  // the text byte before the segment
+    // A: all five start states
+    {
+        uint32_t st[5] = {0, 1, 2, 3, 4}, cnt[5] = {0, 0, 0, 0, 0};
+        uint32_t prevb = before;
+        uint32_t i = a;
+        bool met = false;
+        uint4 q = tx.load(a), nq = tx.load(a + 16);
+        for (; i < b && !met; i += 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (i + j < b) {
+                    const uint32_t c = chunk_byte(q, j);
+                    const bool eq = c == prevb;
+#pragma unroll
+                    for (int p = 0; p < 5; ++p) {
+                        const bool c4 = st[p] == 4;
+                        cnt[p] += c4 ? c : 1u;
+                        st[p] = c4 ? 0u : ((st[p] == 0 || !eq) ? 1u : st[p] + 1u);
+                    }
+                    prevb = c;
+                }
+            }
+            q = nq;
+            nq = tx.load(i + 32);
+            met = st[0] == st[1] && st[0] == st[2] && st[0] == st[3] && st[0] == st[4];
         }
-    };
-    for (uint32_t i0 = 0; i0 < n; i0 += 16) {
-        const uint4 v4 = *(const uint4*)(rle + i0);
-        const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
-        const uint32_t m = min(16u, n - i0);
-        for (uint32_t q = 0; q < m; ++q) {
-            const uint32_t b = (w[q >> 2] >> (8 * (q & 3))) & 255u;
-            if (cnt == 4) {  // the count byte after 4 equal bytes
-                for (uint32_t k = 0; k < b; ++k) put(prev);
-                cnt = 0;
-                prev = 256;
-                continue;
+        // the paths have met (or the segment is done): one path for the rest
+        uint32_t s1 = st[0], c1 = 0;
+        for (; i < b; i += 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (i + j < b) {
+                    const uint32_t c = chunk_byte(q, j);
+                    const bool c4 = s1 == 4;
+                    c1 += c4 ? c : 1u;
+                    s1 = c4 ? 0u : ((s1 == 0 || c != prevb) ? 1u : s1 + 1u);
+                    prevb = c;
+                }
             }
-            put(b);
-            if (b == prev) ++cnt;
-            else {
-                prev = b;
-                cnt = 1;
+            q = nq;
+            nq = tx.load(i + 32);
+        }
+        uint32_t map = 0;
+#pragma unroll
+        for (int p = 0; p < 5; ++p) {
+            map |= (met ? s1 : st[p]) << (3 * p);
+            scnt[p][lane] = cnt[p] + c1;
+        }
+        smap[lane] = map;
+    }
+    __syncthreads();
+    // B: chain the lanes
+    if (lane == 0) {
+        uint32_t stt = 0, off = 0;
+        for (uint32_t l = 0; l < 64; ++l) {
+            sst[l] = stt;
+            soff[l] = off;
+            off += scnt[stt][l];
+            stt = (smap[l] >> (3 * stt)) & 7u;
+        }
+        s_total = off;
+    }
+    __syncthreads();
+    const uint32_t tot = s_total;
+    if (tot > cap) {
+        if (lane == 0) {
+            D.out_len[s] = tot;
+            D.flags[s] = kHost;
+        }
+        return;
+    }
+    // C: decode the segment from its start state
+    {
+        uint32_t s1 = sst[lane], o = soff[lane], prevb = before;
+        uint4 q = tx.load(a), nq = tx.load(a + 16);
+        for (uint32_t i = a; i < b; i += 16) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (i + j < b) {
+                    const uint32_t c = chunk_byte(q, j);
+                    if (s1 == 4) {  // count byte: c more copies of the previous byte
+                        for (uint32_t k = 0; k < c; ++k) out[o + k] = (uint8_t)prevb;
+                        o += c;
+                        s1 = 0;
+                    } else {
+                        out[o++] = (uint8_t)c;
+                        s1 = (s1 == 0 || c != prevb) ? 1u : s1 + 1u;
+                    }
+                    prevb = c;
+                }
             }
+            q = nq;
+            nq = tx.load(i + 32);
         }
     }
-    for (uint32_t k = 0; k < na; ++k)  // bytes left over: one at a time
-        crc = (crc << 8) ^ c_dcrc[(crc >> 24) ^ ((acc >> (8 * (na - 1 - k))) & 255u)];
-    crc = ~crc;
-    D.out_len[s] = o;
-    if (o > cap) D.flags[s] = kHost;
-    else if (crc != D.crc[s]) D.flags[s] = kCrcFail;
+    // the other lanes' bytes are read back below (same wave, L1 write-through)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __syncthreads();
+    // CRC: 64 segments of segc bytes aligned to the end of the output
+    const uint32_t segc = (tot + 63) / 64;
+    const int64_t e = (int64_t)tot - (int64_t)(63 - lane) * segc;
+    const uint32_t c0 = (uint32_t)max<int64_t>(0, e - (int64_t)segc), c1 = (uint32_t)max<int64_t>(0, e);
+    uint32_t r = 0;
+    {  // aligned words (the word holding a valid byte lies in its page)
+        uint32_t w = 0;
+        for (uint32_t i = c0; i < c1; ++i) {
+            const uintptr_t ua = (uintptr_t)(out + i);
+            if (i == c0 || (ua & 3) == 0) w = *(const uint32_t*)(ua & ~(uintptr_t)3);
+            const uint32_t c = (w >> (8 * (ua & 3))) & 0xFFu;
+            r = (r << 8) ^ T1[(r >> 24) ^ c];
+        }
+    }
+    uint32_t X = crc_xpow8(segc);  // wave-uniform
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t left = __shfl_up(r, 1u << j);
+        if (((lane + 1) & ((2u << j) - 1)) == 0) r = crc_mulmod(left, X) ^ r;
+        X = crc_mulmod(X, X);
+    }
+    if (lane == 63) {
+        const uint32_t crc = ~(crc_mulmod(0xFFFFFFFFu, crc_xpow8(tot)) ^ r);
+        D.out_len[s] = tot;
+        if (crc != D.crc[s]) D.flags[s] = kCrcFail;
+    }
 }
 
 } // namespace bzd
@@ -642,6 +782,7 @@ uint32_t dec_cap(uint32_t out_stride)
 uint32_t mark_cap(uint32_t cap) { return (cap + kMark - 1) / kMark + 2; }
 
 uint32_t host_dcrc[256];
+uint32_t host_xpow[24];
 bool dcrc_ready = false;
 
 } // namespace
@@ -676,13 +817,25 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
             for (int k = 0; k < 8; ++k) c = (c & 0x80000000u) ? (c << 1) ^ 0x04c11db7u : (c << 1);
             host_dcrc[i] = c;
         }
+        auto mulmod = [](uint32_t x, uint32_t y) {
+            uint32_t r = 0;
+            for (int i = 31; i >= 0; --i) {
+                r = (r << 1) ^ ((r >> 31) ? 0x04C11DB7u : 0u);
+                if ((y >> i) & 1u) r ^= x;
+            }
+            return r;
+        };
+        host_xpow[0] = 0x100u;  // x^8
+        for (int k = 1; k < 24; ++k) host_xpow[k] = mulmod(host_xpow[k - 1], host_xpow[k - 1]);
         dcrc_ready = true;
     }
     static thread_local int crc_dev = -1;
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (crc_dev != dev) {
-        if (hipMemcpyToSymbol(HIP_SYMBOL(c_dcrc), host_dcrc, sizeof(host_dcrc)) != hipSuccess) return LFM_HIP_ERUNTIME;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_dcrc), host_dcrc, sizeof(host_dcrc)) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(c_xpow), host_xpow, sizeof(host_xpow)) != hipSuccess)
+            return LFM_HIP_ERUNTIME;
         crc_dev = dev;
     }
     Dec D{};
@@ -707,7 +860,6 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     (void)take((size_t)count * 4 + 64);
     if (hipMemcpyAsync(d_offs, h_offs, ((size_t)count + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
-    const uint32_t g64 = (count + 63) / 64;
     D.sel_cap = std::min<uint32_t>(kMaxSel, (D.cap + 49) / 50 + 64);
     const size_t sel_lds = ((D.sel_cap + 7) / 8 * 4 + 15) & ~(size_t)15;
     static const int lut_bits = [] {
@@ -720,7 +872,7 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     else hipLaunchKernelGGL(bzd_huff<8>, dim3(count), dim3(64), sel_lds, st, D);
     hipLaunchKernelGGL(bzd_tt, dim3(count), dim3(kTtThreads), 0, st, D);
     hipLaunchKernelGGL(bzd_walk, dim3(count), dim3(kTtThreads), 0, st, D);
-    hipLaunchKernelGGL(bzd_rle1, dim3(g64), dim3(64), 0, st, D);
+    hipLaunchKernelGGL(bzd_rle1, dim3(count), dim3(64), 0, st, D);
     if (hipGetLastError() != hipSuccess) return LFM_HIP_ERUNTIME;
     if (hipMemcpyAsync(h_lens, D.out_len, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(h_flags, D.flags, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||

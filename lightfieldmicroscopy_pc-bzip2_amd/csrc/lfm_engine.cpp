@@ -1000,6 +1000,18 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     const size_t bpp = h.getBytesPerPixel();
     const uint32_t block_bytes = h.getBlockSizeBytes();
     if (!nb || !block_bytes || nb >= (1ull << 31)) return -1;
+    // LFM_DECODE_TIMING=1: phase times on stderr (synchronizes between phases)
+    static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
+    auto tp = std::chrono::steady_clock::now();
+    hipStream_t st = nullptr;
+    auto phase = [&](const char* name) {
+        if (!timing) return;
+        if (st) (void)hipStreamSynchronize(st);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "decode phase %-10s %8.2f ms\n", name,
+                     std::chrono::duration<double, std::milli>(now - tp).count());
+        tp = now;
+    };
     std::vector<uint64_t> offs(nb + 1);
     for (uint64_t i = 0; i < nb; ++i) {
         offs[i] = h.getBlockOffset(i);
@@ -1012,7 +1024,6 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     const size_t budget = (size_t)env_int("LFM_BUNZIP2_GPU_BUDGET_MB", 16 * 1024) << 20;
     const uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nb, budget / per));
     const size_t ws = lfm_hip_bunzip2_workspace_bytes((uint32_t)batch, block_bytes);
-    hipStream_t st = nullptr;
     void *d_pay = nullptr, *d_ws = nullptr, *d_blk = nullptr, *d_sym = nullptr, *d_out = nullptr;
     auto release = [&]() {
         for (void* q : {d_pay, d_ws, d_blk, d_sym, d_out})
@@ -1026,10 +1037,12 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
         release();
         return -1;
     }
+    phase("alloc");
     int rc = 0;
     if (hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, st) != hipSuccess)
         rc = 3;
+    phase("upload");
     uint32_t dims[5], bs[5];
     for (int d = 0; d < 5; ++d) {
         dims[d] = h.xyzct[d];
@@ -1044,6 +1057,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             rc = 3;
             break;
         }
+        phase("bunzip2");
         for (uint32_t i = 0; i < cnt && !rc; ++i) {
             uint64_t o[5], sz[5];
             g.block(b0 + i, o, sz);
@@ -1066,6 +1080,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                        LFM_HIP_OK)
             rc = 3;
     }
+    phase("scatter");
     if (!rc && predicted) {
         const int W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
         const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
@@ -1082,10 +1097,13 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             }
         }
     }
+    phase("unpredict");
     if (!rc && (hipMemcpyAsync(img, predicted ? d_out : d_sym, img_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess))
         rc = 3;
+    phase("download");
     release();
+    phase("free");
     return rc;
 }
 
