@@ -986,6 +986,99 @@ void parallel_for(uint64_t n, int threads, F&& f)
     w();
     for (auto& t : pool) t.join();
 }
+
+// Host <-> device copies of pageable buffers through two pinned staging
+// chunks: the DMA of one chunk overlaps the multi-threaded host copy of the
+// other (the runtime's own staging copies with one thread and takes the page
+// faults of a fresh destination on that thread).  The pinned chunks and their
+// events are kept per host thread and device.
+struct Staging {
+    static constexpr size_t kChunk = 32u << 20;
+    void* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    int dev = -1;
+    bool ready()
+    {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (dev == d && buf[0]) return true;
+        for (int i = 0; i < 2; ++i) {
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            ev[i] = nullptr;
+            if (!buf[i] && hipHostMalloc(&buf[i], kChunk, hipHostMallocPortable) != hipSuccess) {
+                buf[i] = nullptr;
+                return false;
+            }
+            if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return false;
+        }
+        dev = d;
+        return true;
+    }
+};
+
+Staging& staging()
+{
+    static thread_local Staging s;  // the pinned chunks stay for the thread's life
+    return s;
+}
+
+void par_memcpy(void* dst, const void* src, size_t n, int threads)
+{
+    const size_t piece = 1u << 20;
+    const uint64_t np = (n + piece - 1) / piece;
+    if (threads <= 1 || np <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    parallel_for(np, threads, [&](uint64_t i) {
+        const size_t o = i * piece;
+        std::memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(piece, n - o));
+    });
+}
+
+bool staged_h2d(void* d_dst, const void* h_src, size_t n, hipStream_t st, int threads)
+{
+    Staging& S = staging();
+    if (!S.ready()) return hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, st) == hipSuccess;
+    for (size_t off = 0, i = 0; off < n; off += Staging::kChunk, ++i) {
+        const int b = (int)(i & 1);
+        const size_t len = std::min(Staging::kChunk, n - off);
+        if (S.used[b] && hipEventSynchronize(S.ev[b]) != hipSuccess) return false;
+        par_memcpy(S.buf[b], (const uint8_t*)h_src + off, len, threads);
+        if (hipMemcpyAsync((uint8_t*)d_dst + off, S.buf[b], len, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(S.ev[b], st) != hipSuccess)
+            return false;
+        S.used[b] = true;
+    }
+    return true;
+}
+
+bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads)
+{
+    Staging& S = staging();
+    if (!S.ready())
+        return hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, st) == hipSuccess &&
+               hipStreamSynchronize(st) == hipSuccess;
+    const size_t nc = (n + Staging::kChunk - 1) / Staging::kChunk;
+    auto issue = [&](size_t i) {
+        const int b = (int)(i & 1);
+        const size_t off = i * Staging::kChunk, len = std::min(Staging::kChunk, n - off);
+        S.used[b] = true;
+        return hipMemcpyAsync(S.buf[b], (const uint8_t*)d_src + off, len, hipMemcpyDeviceToHost, st) == hipSuccess &&
+               hipEventRecord(S.ev[b], st) == hipSuccess;
+    };
+    for (size_t i = 0; i < std::min<size_t>(2, nc); ++i)
+        if (!issue(i)) return false;
+    for (size_t i = 0; i < nc; ++i) {
+        const int b = (int)(i & 1);
+        const size_t off = i * Staging::kChunk, len = std::min(Staging::kChunk, n - off);
+        if (hipEventSynchronize(S.ev[b]) != hipSuccess) return false;
+        par_memcpy((uint8_t*)h_dst + off, S.buf[b], len, threads);
+        if (i + 2 < nc && !issue(i + 2)) return false;
+    }
+    return true;
+}
 } // namespace
 
 // GPU decode of a BZIP2 payload (lfm_bunzip2.hip): payload up, streams decoded
@@ -993,7 +1086,7 @@ void parallel_for(uint64_t n, int threads, F&& f)
 // library), inverse predictor on the device, image down.  Returns -1 when the
 // GPU path does not apply (the caller decodes on the host).
 static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int family,
-                      bool predicted, int k, int video)
+                      bool predicted, int k, int video, int threads)
 {
     const BlockGrid g(h);
     const uint64_t nb = g.nblocks;
@@ -1039,7 +1132,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     }
     phase("alloc");
     int rc = 0;
-    if (hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) != hipSuccess ||
+    if (!staged_h2d(d_pay, payload, offs[nb], st, threads) ||
         hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, st) != hipSuccess)
         rc = 3;
     phase("upload");
@@ -1098,7 +1191,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
         }
     }
     phase("unpredict");
-    if (!rc && (hipMemcpyAsync(img, predicted ? d_out : d_sym, img_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (!rc && (!staged_d2h(img, predicted ? d_out : d_sym, img_bytes, st, threads) ||
                 hipStreamSynchronize(st) != hipSuccess))
         rc = 3;
     phase("download");
@@ -1124,7 +1217,7 @@ int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h
     }
     if (h.compressionType == BZIP2 && gpu_decode_enabled() && gpu_bunzip2_enabled() && lfm_hip_device_count() > 0 &&
         (!predicted || h.Nnum <= 31)) {
-        const int rc = gpu_decode(payload, len, h, img, family, predicted, k, video);
+        const int rc = gpu_decode(payload, len, h, img, family, predicted, k, video, threads);
         if (rc != -1) return rc;
     }
     std::vector<uint16_t> symbuf;
