@@ -59,7 +59,7 @@ struct Dec {
     uint8_t* out;
     uint8_t* ll;              // cap per stream
     uint32_t* tt;             // cap per stream
-    uint8_t* rle;             // cap per stream
+    uint8_t* rle;             // cap per stream (the same buffer as ll)
     uint32_t mcap;            // markers per stream
     uint32_t* mnext;
     uint32_t* mlen;
@@ -792,9 +792,8 @@ extern "C" size_t lfm_hip_bunzip2_workspace_bytes(uint32_t count, uint32_t out_s
     const size_t cap = dec_cap(out_stride), mc = mark_cap((uint32_t)cap);
     size_t b = 0;
     b += al(((size_t)count + 1) * 8);
-    b += al((size_t)count * cap);          // ll
+    b += al((size_t)count * cap);          // ll, then the RLE1 text (ll is dead once tt holds its bytes)
     b += al((size_t)count * cap * 4);      // tt
-    b += al((size_t)count * cap);          // rle
     b += 3 * al((size_t)count * mc * 4);
     b += 6 * al((size_t)count * 4 + 64);
     return b;
@@ -851,7 +850,7 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     D.offs = d_offs;
     D.ll = take((size_t)count * D.cap);
     D.tt = (uint32_t*)take((size_t)count * D.cap * 4);
-    D.rle = take((size_t)count * D.cap);
+    D.rle = D.ll;  // bzd_walk writes the text over ll (bzd_tt copied ll into tt)
     D.mnext = (uint32_t*)take((size_t)count * D.mcap * 4);
     D.mlen = (uint32_t*)take((size_t)count * D.mcap * 4);
     D.mstart = (uint32_t*)take((size_t)count * D.mcap * 4);

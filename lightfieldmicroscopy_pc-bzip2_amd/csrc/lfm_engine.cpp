@@ -1041,11 +1041,22 @@ bool staged_h2d(void* d_dst, const void* h_src, size_t n, hipStream_t st, int th
 {
     Staging& S = staging();
     if (!S.ready()) return hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, st) == hipSuccess;
+    static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
+    double t_wait = 0, t_copy = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
     for (size_t off = 0, i = 0; off < n; off += Staging::kChunk, ++i) {
         const int b = (int)(i & 1);
         const size_t len = std::min(Staging::kChunk, n - off);
+        auto t0 = now();
         if (S.used[b] && hipEventSynchronize(S.ev[b]) != hipSuccess) return false;
+        auto t1 = now();
         par_memcpy(S.buf[b], (const uint8_t*)h_src + off, len, threads);
+        auto t2 = now();
+        t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        t_copy += std::chrono::duration<double, std::milli>(t2 - t1).count();
+        if (timing && off + len >= n)
+            std::fprintf(stderr, "staged h2d: %zu bytes, host copies %.2f ms, waits %.2f ms, %d threads\n", n, t_copy,
+                         t_wait, threads);
         if (hipMemcpyAsync((uint8_t*)d_dst + off, S.buf[b], len, hipMemcpyHostToDevice, st) != hipSuccess ||
             hipEventRecord(S.ev[b], st) != hipSuccess)
             return false;
@@ -1079,6 +1090,63 @@ bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int th
     }
     return true;
 }
+
+// Device buffers and stream of the GPU decode, kept per host thread and
+// device between calls (LFM_DECODE_KEEP=0 releases them after every call):
+// fresh device allocations are cleared by the driver before first use, which
+// showed up as 20-40 ms stalls of the first upload.
+struct DecodeBuffers {
+    enum { PAY, WS, BLK, SYM, OUT, N };
+    int dev = -1;
+    hipStream_t st = nullptr;
+    void* p[N] = {};
+    size_t cap[N] = {};
+    void release()
+    {
+        for (int i = 0; i < N; ++i) {
+            if (p[i]) (void)hipFree(p[i]);
+            p[i] = nullptr;
+            cap[i] = 0;
+        }
+        if (st) (void)hipStreamDestroy(st);
+        st = nullptr;
+        dev = -1;
+    }
+    bool begin()
+    {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (dev != d) {
+            release();
+            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+                st = nullptr;
+                return false;
+            }
+            dev = d;
+        }
+        return true;
+    }
+    void* get(int i, size_t bytes)
+    {
+        if (cap[i] >= bytes) return p[i];
+        if (p[i]) (void)hipFree(p[i]);
+        p[i] = nullptr;
+        cap[i] = 0;
+        if (hipMalloc(&p[i], bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            p[i] = nullptr;
+            return nullptr;
+        }
+        cap[i] = bytes;
+        return p[i];
+    }
+};
+
+DecodeBuffers& decode_buffers()
+{
+    static thread_local DecodeBuffers b;
+    return b;
+}
 } // namespace
 
 // GPU decode of a BZIP2 payload (lfm_bunzip2.hip): payload up, streams decoded
@@ -1096,6 +1164,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     // LFM_DECODE_TIMING=1: phase times on stderr (synchronizes between phases)
     static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
     auto tp = std::chrono::steady_clock::now();
+    DecodeBuffers& DB = decode_buffers();
     hipStream_t st = nullptr;
     auto phase = [&](const char* name) {
         if (!timing) return;
@@ -1117,17 +1186,21 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     const size_t budget = (size_t)env_int("LFM_BUNZIP2_GPU_BUDGET_MB", 16 * 1024) << 20;
     const uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nb, budget / per));
     const size_t ws = lfm_hip_bunzip2_workspace_bytes((uint32_t)batch, block_bytes);
-    void *d_pay = nullptr, *d_ws = nullptr, *d_blk = nullptr, *d_sym = nullptr, *d_out = nullptr;
+    static const bool keep = env_int("LFM_DECODE_KEEP", 1) != 0;
     auto release = [&]() {
-        for (void* q : {d_pay, d_ws, d_blk, d_sym, d_out})
-            if (q) (void)hipFree(q);
-        if (st) (void)hipStreamDestroy(st);
+        if (!keep) DB.release();
     };
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess || hipMalloc(&d_pay, offs[nb] + 64) != hipSuccess ||
-        hipMalloc(&d_ws, ws) != hipSuccess || hipMalloc(&d_blk, batch * block_bytes) != hipSuccess ||
-        hipMalloc(&d_sym, img_bytes) != hipSuccess || (predicted && hipMalloc(&d_out, img_bytes) != hipSuccess)) {
-        (void)hipGetLastError();
-        release();
+    void *d_pay = nullptr, *d_ws = nullptr, *d_blk = nullptr, *d_sym = nullptr, *d_out = nullptr;
+    if (DB.begin()) {
+        st = DB.st;
+        d_pay = DB.get(DecodeBuffers::PAY, offs[nb] + 64);
+        d_ws = DB.get(DecodeBuffers::WS, ws);
+        d_blk = DB.get(DecodeBuffers::BLK, batch * block_bytes);
+        d_sym = DB.get(DecodeBuffers::SYM, img_bytes);
+        d_out = predicted ? DB.get(DecodeBuffers::OUT, img_bytes) : nullptr;
+    }
+    if (!st || !d_pay || !d_ws || !d_blk || !d_sym || (predicted && !d_out)) {
+        DB.release();
         return -1;
     }
     phase("alloc");

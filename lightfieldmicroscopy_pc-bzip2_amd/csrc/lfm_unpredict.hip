@@ -254,6 +254,151 @@ __device__ __forceinline__ void band2(const UnFrames& p, int fz, uint16_t* ring,
     }
 }
 
+// band3: the band2 wavefront with the step's dependency chain cut down to
+// registers.  The neighbours one step away come from registers: A = this
+// lane's previous result, B / C = row r - 1's previous / second-previous
+// result moved over by a DPP lane shift (row 0 takes them from `top`); every
+// other neighbour was produced at least T steps earlier and is read from LDS
+// before the step's own writes.  Outside the first band and the first T + 63
+// steps of a band every lane is in the interior tile case, so the four
+// position-case formulas are all evaluated and one is selected per lane (no
+// divergent case switch); the edge steps run the per-lane switch.
+struct NbVals {
+    int v[NB_COUNT];
+    template <int N>
+    __device__ __forceinline__ int at() const { return v[N]; }
+};
+
+template <int FAM, int K, int TC, int UC, bool TEMP>
+__device__ __forceinline__ int inv_case3(NbVals& g, int r, int P)
+{
+    constexpr int F = case_formula(FAM, K, TC, UC);
+    const int pr = eval_formula<F>(g);
+    if constexpr (!TEMP) return r + pr;
+    else if constexpr (F == F_Z) return r + P;
+    else return r + ((pr + P) >> 1);
+}
+
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ int inv_any3(NbVals& g, int tc, int uc, int res, int P)
+{
+    switch (tc * 4 + uc) {
+#define LFM_INV(TC_, UC_) case TC_ * 4 + UC_: return inv_case3<FAM, K, TC_, UC_, TEMP>(g, res, P);
+    LFM_INV(0, 0) LFM_INV(0, 1) LFM_INV(0, 2) LFM_INV(0, 3)
+    LFM_INV(1, 0) LFM_INV(1, 1) LFM_INV(1, 2) LFM_INV(1, 3)
+    LFM_INV(2, 0) LFM_INV(2, 1) LFM_INV(2, 2) LFM_INV(2, 3)
+    LFM_INV(3, 0) LFM_INV(3, 1) LFM_INV(3, 2) LFM_INV(3, 3)
+#undef LFM_INV
+    }
+    return 0;
+}
+
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring, uint16_t* top)
+{
+    const int r = threadIdx.x;
+    const size_t fs = (size_t)p.W * p.H;
+    const uint16_t* sym = p.sym + fz * fs;
+    uint16_t* out = p.out + fz * fs;
+    const uint16_t* prev = TEMP ? (fz ? p.out + (fz - 1) * fs : p.prev) : nullptr;
+    const int W = p.W, H = p.H, T = p.T, TT = T + 1, tb = 64 - TT;
+    // LDS offset (u16 units, relative to ring) of neighbour (x + dx, y + dy)
+    auto far = [&](int x, int dx, int dy) -> int {
+        const int rr = r + dy;
+        return rr >= 0 ? rr * kRing + ((x + dx) & (kRing - 1)) : 64 * kRing + (TT + rr) * W + (x + dx);
+    };
+    for (int y0 = 0; y0 < H; y0 += 64) {
+        const int y = y0 + r;
+        const bool row_ok = y < H;
+        const int v = y % T, ty = y / T;
+        const uint16_t* srow = sym + (size_t)(row_ok ? y : 0) * W;
+        const uint16_t* prow = TEMP ? prev + (size_t)(row_ok ? y : 0) * W : nullptr;
+        uint16_t* orow = out + (size_t)(row_ok ? y : 0) * W;
+        uint16_t* trow = top + (r >= tb ? r - tb : 0) * W;
+        const uint16_t* btop = top + (TT - 1) * W;  // the previous band's last row (row 0's B and C)
+        // delay lines: symbol (and previous-frame pixel) of column k - r for
+        // the step k = k0 + j of the current round
+        uint32_t sq[kSymAhead], pq[kSymAhead];
+#pragma unroll
+        for (int j = 0; j < kSymAhead; ++j) {
+            const int x = min(max(j - r, 0), W - 1);
+            sq[j] = srow[x];
+            pq[j] = TEMP ? prow[x] : 0u;
+        }
+        int u = 0, tx = 0;  // x % T and x / T, advanced with x
+        int p1 = 0, p2 = 0; // this lane's results of the last two steps
+        const int edge_k = y0 == 0 ? 1 << 30 : T + 63;  // steps before this run the case switch
+        for (int k0 = 0; k0 < W + 63; k0 += kSymAhead) {
+#pragma unroll
+            for (int j = 0; j < kSymAhead; ++j) {
+                const int k = k0 + j;
+                const int x = k - r;
+                const uint32_t sv = sq[j], pv = pq[j];
+                {  // the loads for step k + kSymAhead (column x + kSymAhead):
+                    // clamped and unconditional, so their wait lands at their use
+                    const int xn = min(max(x + kSymAhead, 0), W - 1);
+                    sq[j] = srow[xn];
+                    if (TEMP) pq[j] = prow[xn];
+                }
+                const bool ok = row_ok && x >= 0 && x < W;
+                NbVals g;
+                {
+                    const int bt = r == 0 && x >= 0 ? (int)btop[x] : 0;
+                    const int ct = r == 0 && x >= 1 ? (int)btop[x - 1] : 0;
+                    g.v[NB_A] = p1;
+                    g.v[NB_B] = __builtin_amdgcn_update_dpp(bt, p1, 0x138, 0xF, 0xF, false);
+                    g.v[NB_C] = __builtin_amdgcn_update_dpp(ct, p2, 0x138, 0xF, 0xF, false);
+                    g.v[NB_AP] = ring[far(x, -T, 0)];
+                    g.v[NB_BP] = ring[far(x, 0, -T)];
+                    g.v[NB_CP] = ring[far(x, -T, -T)];
+                    g.v[NB_AP1] = ring[far(x, -TT, 0)];
+                    g.v[NB_BP1] = ring[far(x, 0, -TT)];
+                    g.v[NB_ABP] = ring[far(x, -1, -T)];
+                    g.v[NB_BAP] = ring[far(x, -T, -1)];
+                }
+                const int res = unsymbolize16(sv);
+                const int P = TEMP ? (int)pv : 0;
+                int val;
+                if (k >= edge_k) {  // every valid lane: tile case XY
+                    const int vc = inv_case3<FAM, K, TC_XY, UC_COL, TEMP>(g, res, P);
+                    const int vk = inv_case3<FAM, K, TC_XY, UC_CORNER, TEMP>(g, res, P);
+                    const int vr = inv_case3<FAM, K, TC_XY, UC_ROW, TEMP>(g, res, P);
+                    const int vi = inv_case3<FAM, K, TC_XY, UC_IN, TEMP>(g, res, P);
+                    val = u == 0 ? (v > 0 ? vc : vk) : (v == 0 ? vr : vi);
+                } else {
+                    const int tc = tx == 0 ? (ty == 0 ? TC_00 : TC_0Y) : (ty == 0 ? TC_X0 : TC_XY);
+                    const int uc = u == 0 ? (v > 0 ? UC_COL : UC_CORNER) : (v == 0 ? UC_ROW : UC_IN);
+                    val = ok ? inv_any3<FAM, K, TEMP>(g, tc, uc, res, P) : 0;
+                }
+                const uint16_t o = (uint16_t)val;
+                if (ok) {
+                    ring[r * kRing + (x & (kRing - 1))] = o;
+                    orow[x] = o;
+                    if (r >= tb) trow[x] = o;
+                    if (++u == T) {
+                        u = 0;
+                        ++tx;
+                    }
+                }
+                p2 = p1;
+                p1 = (int)o;
+            }
+        }
+    }
+}
+
+template <int FAM, int K>
+__global__ __launch_bounds__(64) void unpredict_band3(UnFrames p)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds3[];
+    const int fz = p.first + (int)blockIdx.x * p.step;
+    if (fz >= p.nz) return;
+    uint16_t* ring = lds3;
+    uint16_t* top = lds3 + 64 * kRing;
+    if (p.video && ((p.z0 + fz) & 1)) band3<FAM, K, true>(p, fz, ring, top);
+    else band3<FAM, K, false>(p, fz, ring, top);
+}
+
 template <int FAM, int K>
 __global__ __launch_bounds__(64) void unpredict_band2(UnFrames p)
 {
@@ -277,10 +422,12 @@ template <int FAM, int K_>
 static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
 {
     const size_t lds = band2_lds(p);
-    const void* fn = (const void*)unpredict_band2<FAM, K_>;
+    static const bool v2 = std::getenv("LFM_UNPREDICT_V2") != nullptr;
+    const void* fn = v2 ? (const void*)unpredict_band2<FAM, K_> : (const void*)unpredict_band3<FAM, K_>;
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL((unpredict_band2<FAM, K_>), dim3(grid), dim3(64), lds, st, p);
+    if (v2) hipLaunchKernelGGL((unpredict_band2<FAM, K_>), dim3(grid), dim3(64), lds, st, p);
+    else hipLaunchKernelGGL((unpredict_band3<FAM, K_>), dim3(grid), dim3(64), lds, st, p);
     return hipGetLastError();
 }
 
