@@ -327,6 +327,21 @@ __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring,
         }
         int u = 0, tx = 0;  // x % T and x / T, advanced with x
         int p1 = 0, p2 = 0; // this lane's results of the last two steps
+        // far neighbours of column x (B / C slots: row 0's values from `top`)
+        auto load_far = [&](NbVals& f, int x) {
+            f.v[NB_B] = r == 0 && x >= 0 ? (int)btop[x] : 0;
+            f.v[NB_C] = r == 0 && x >= 1 ? (int)btop[x - 1] : 0;
+            f.v[NB_AP] = ring[far(x, -T, 0)];
+            f.v[NB_BP] = ring[far(x, 0, -T)];
+            f.v[NB_CP] = ring[far(x, -T, -T)];
+            f.v[NB_AP1] = ring[far(x, -TT, 0)];
+            f.v[NB_BP1] = ring[far(x, 0, -TT)];
+            f.v[NB_ABP] = ring[far(x, -1, -T)];
+            f.v[NB_BAP] = ring[far(x, -T, -1)];
+        };
+        NbVals nf;
+        nf.v[NB_A] = 0;
+        load_far(nf, -r);
         const int edge_k = y0 == 0 ? 1 << 30 : T + 63;  // steps before this run the case switch
         for (int k0 = 0; k0 < W + 63; k0 += kSymAhead) {
 #pragma unroll
@@ -341,21 +356,13 @@ __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring,
                     if (TEMP) pq[j] = prow[xn];
                 }
                 const bool ok = row_ok && x >= 0 && x < W;
-                NbVals g;
-                {
-                    const int bt = r == 0 && x >= 0 ? (int)btop[x] : 0;
-                    const int ct = r == 0 && x >= 1 ? (int)btop[x - 1] : 0;
-                    g.v[NB_A] = p1;
-                    g.v[NB_B] = __builtin_amdgcn_update_dpp(bt, p1, 0x138, 0xF, 0xF, false);
-                    g.v[NB_C] = __builtin_amdgcn_update_dpp(ct, p2, 0x138, 0xF, 0xF, false);
-                    g.v[NB_AP] = ring[far(x, -T, 0)];
-                    g.v[NB_BP] = ring[far(x, 0, -T)];
-                    g.v[NB_CP] = ring[far(x, -T, -T)];
-                    g.v[NB_AP1] = ring[far(x, -TT, 0)];
-                    g.v[NB_BP1] = ring[far(x, 0, -TT)];
-                    g.v[NB_ABP] = ring[far(x, -1, -T)];
-                    g.v[NB_BAP] = ring[far(x, -T, -1)];
-                }
+                // this step's far neighbours were read during the last step
+                // (T >= 2: nothing they need is written by that step)
+                NbVals g = nf;
+                load_far(nf, x + 1);
+                g.v[NB_A] = p1;
+                g.v[NB_B] = __builtin_amdgcn_update_dpp(g.v[NB_B], p1, 0x138, 0xF, 0xF, false);
+                g.v[NB_C] = __builtin_amdgcn_update_dpp(g.v[NB_C], p2, 0x138, 0xF, 0xF, false);
                 const int res = unsymbolize16(sv);
                 const int P = TEMP ? (int)pv : 0;
                 int val;
@@ -422,7 +429,9 @@ template <int FAM, int K_>
 static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
 {
     const size_t lds = band2_lds(p);
-    static const bool v2 = std::getenv("LFM_UNPREDICT_V2") != nullptr;
+    // band3 reads a step's far neighbours one step early: T >= 2
+    static const bool v2_env = std::getenv("LFM_UNPREDICT_V2") != nullptr;
+    const bool v2 = v2_env || p.T < 2;
     const void* fn = v2 ? (const void*)unpredict_band2<FAM, K_> : (const void*)unpredict_band3<FAM, K_>;
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return hipErrorInvalidValue;
