@@ -51,30 +51,10 @@ int klb_imageIO::readImageFull(char* img, int nThreads)
 
 int klb_imageIO::readImage(char* img, const klb_ROI* roi, int nThreads)
 {
-    // decode the whole image, then crop (the reference's block-ROI path cannot
-    // undo predictors, klb_imageIO.cpp:2614-2682)
-    if (filename.empty()) return 3;
-    std::vector<uint8_t> full;
-    int rc = lfm::decode_file(filename.c_str(), header, &full, nullptr, nThreads);
-    if (rc) return rc;
-    const size_t bpp = header.getBytesPerPixel();
-    uint64_t lb[5], ub[5], stride[5], s = 1;
-    for (int d = 0; d < 5; ++d) {
-        lb[d] = roi->xyzctLB[d];
-        ub[d] = roi->xyzctUB[d];
-        if (ub[d] < lb[d] || ub[d] >= header.xyzct[d]) return 3;
-        stride[d] = s;
-        s *= header.xyzct[d];
-    }
-    const size_t row = (ub[0] - lb[0] + 1) * bpp;
-    uint8_t* out = (uint8_t*)img;
-    for (uint64_t t = lb[4]; t <= ub[4]; ++t)
-        for (uint64_t c = lb[3]; c <= ub[3]; ++c)
-            for (uint64_t z = lb[2]; z <= ub[2]; ++z)
-                for (uint64_t y = lb[1]; y <= ub[1]; ++y) {
-                    const uint64_t e = lb[0] + y * stride[1] + z * stride[2] + c * stride[3] + t * stride[4];
-                    std::memcpy(out, full.data() + e * bpp, row);
-                    out += row;
-                }
-    return 0;
+    // decode the blocks the ROI depends on (all of them up / left of it in its
+    // frames when predictors are on), then crop: lfm::decode_roi.  The
+    // reference's block-ROI path cannot undo predictors (klb_imageIO.cpp:2614-2682)
+    if (filename.empty() || !roi) return 3;
+    if (nThreads <= 0) nThreads = lfm::default_threads();
+    return lfm::decode_file_roi(filename.c_str(), header, roi->xyzctLB, roi->xyzctUB, (uint8_t*)img, nThreads);
 }

@@ -1376,6 +1376,106 @@ int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h
     return 0;
 }
 
+// ROI read: decode only the blocks the ROI depends on, then
+// crop.  Every predictor neighbour is up and / or left in its frame, so a
+// predicted ROI needs x in [0, ub0] and y in [0, ub1] of its frames (the
+// inverse on that corner computes the same pixels as on the whole frame);
+// a temporal (odd z) frame of a video stack also needs the frame before it.
+// The blocks of that region (whole blocks, origin z even on video stacks so
+// the temporal parity is unchanged) are described by a sub-header whose block
+// grid is exactly those blocks in file order, their streams are gathered into
+// a sub-payload, and the ordinary decode (GPU or host) runs on it.  The
+// reference's own ROI path decodes the ROI's blocks and then un-predicts them
+// as if they were the whole frame, which is wrong with predictors
+// (klb_imageIO.cpp:2614-2682).
+int decode_roi(const uint8_t* payload, size_t len, const klb_image_header& h, const uint32_t lb[5],
+               const uint32_t ub[5], uint8_t* out, int threads, int family)
+{
+    const BlockGrid g(h);
+    if (g.nblocks != h.Nb) return 3;
+    const size_t bpp = h.getBytesPerPixel();
+    if (!bpp) return 5;
+    for (int d = 0; d < 5; ++d)
+        if (ub[d] < lb[d] || ub[d] >= h.xyzct[d]) return 3;
+    const int k = h.headerVersion & 0x7F;
+    const bool video = (h.headerVersion >> 7) & 1;
+    const bool predicted = bpp == 2 && k != 0;
+    uint64_t b0[5], b1[5], o[5], n[5];
+    for (int d = 0; d < 5; ++d) {
+        uint64_t lo = lb[d];
+        if (predicted && d < 2) lo = 0;
+        if (predicted && video && d == 2 && (lo & 1)) lo -= 1;
+        b0[d] = lo / g.bs[d];
+        b1[d] = ub[d] / g.bs[d] + 1;
+    }
+    if (predicted && video)
+        while (b0[2] > 0 && ((b0[2] * g.bs[2]) & 1)) --b0[2];
+    klb_image_header sub(h);
+    for (int d = 0; d < 5; ++d) {
+        o[d] = b0[d] * g.bs[d];
+        n[d] = std::min<uint64_t>(g.dims[d], b1[d] * g.bs[d]) - o[d];
+        sub.xyzct[d] = (uint32_t)n[d];
+    }
+    const uint64_t cnt = (b1[0] - b0[0]) * (b1[1] - b0[1]) * (b1[2] - b0[2]) * (b1[3] - b0[3]) * (b1[4] - b0[4]);
+    sub.resizeBlockOffset(cnt);
+    std::vector<uint64_t> ids;
+    ids.reserve(cnt);
+    uint64_t total = 0;
+    for (uint64_t t = b0[4]; t < b1[4]; ++t)
+        for (uint64_t c = b0[3]; c < b1[3]; ++c)
+            for (uint64_t z = b0[2]; z < b1[2]; ++z)
+                for (uint64_t y = b0[1]; y < b1[1]; ++y)
+                    for (uint64_t x = b0[0]; x < b1[0]; ++x) {
+                        const uint64_t id = x + g.nb[0] * (y + g.nb[1] * (z + g.nb[2] * (c + g.nb[3] * t)));
+                        const uint64_t e = h.getBlockOffset(id) + h.getBlockCompressedSizeBytes(id);
+                        if (e > len) return 3;
+                        total += h.getBlockCompressedSizeBytes(id);
+                        sub.blockOffset[ids.size()] = total;
+                        ids.push_back(id);
+                    }
+    std::vector<uint8_t> spay(total);
+    parallel_for(ids.size(), threads, [&](uint64_t i) {
+        const uint64_t id = ids[i], sz = h.getBlockCompressedSizeBytes(id);
+        std::memcpy(spay.data() + (sub.blockOffset[i] - sz), payload + h.getBlockOffset(id), sz);
+    });
+    std::vector<uint8_t> simg(sub.getImageSizeBytes());
+    const int rc = decode_payload(spay.data(), spay.size(), sub, simg.data(), threads, family);
+    if (rc) return rc;
+    const size_t row = (size_t)(ub[0] - lb[0] + 1) * bpp;
+    uint8_t* q = out;
+    for (uint64_t t = lb[4]; t <= ub[4]; ++t)
+        for (uint64_t c = lb[3]; c <= ub[3]; ++c)
+            for (uint64_t z = lb[2]; z <= ub[2]; ++z)
+                for (uint64_t y = lb[1]; y <= ub[1]; ++y) {
+                    const uint64_t e = (lb[0] - o[0]) +
+                                       n[0] * ((y - o[1]) + n[1] * ((z - o[2]) + n[2] * ((c - o[3]) + n[3] * (t - o[4]))));
+                    std::memcpy(q, simg.data() + e * bpp, row);
+                    q += row;
+                }
+    return 0;
+}
+
+int decode_file_roi(const char* filename, klb_image_header& h, const uint32_t lb[5], const uint32_t ub[5],
+                    uint8_t* out, int threads)
+{
+    FILE* f = std::fopen(filename, "rb");
+    if (!f) {
+        std::printf("ERROR: file %s could not be opened\n", filename);
+        return 3;
+    }
+    std::fseek(f, 0, SEEK_END);
+    const long size = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    std::vector<uint8_t> buf(size > 0 ? (size_t)size : 0);
+    const size_t got = buf.empty() ? 0 : std::fread(buf.data(), 1, buf.size(), f);
+    std::fclose(f);
+    if (got != buf.size()) return 3;
+    int rc = h.parseHeader(buf.data(), buf.size());
+    if (rc) return rc;
+    const size_t hs = h.getSizeInBytes();
+    return decode_roi(buf.data() + hs, buf.size() - hs, h, lb, ub, out, threads, current_family());
+}
+
 int decode_file(const char* filename, klb_image_header& h, std::vector<uint8_t>* img_out, uint8_t* img_into,
                 int threads)
 {

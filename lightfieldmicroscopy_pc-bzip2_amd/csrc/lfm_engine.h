@@ -155,5 +155,10 @@ int decode_payload(const uint8_t* payload, size_t len, const klb_image_header& h
                    int family);
 int decode_file(const char* filename, klb_image_header& h, std::vector<uint8_t>* img_out, uint8_t* img_into,
                 int threads);
+// ROI read: only the blocks the ROI depends on are decoded (lb / ub inclusive)
+int decode_roi(const uint8_t* payload, size_t len, const klb_image_header& h, const uint32_t lb[5],
+               const uint32_t ub[5], uint8_t* out, int threads, int family);
+int decode_file_roi(const char* filename, klb_image_header& h, const uint32_t lb[5], const uint32_t ub[5],
+                    uint8_t* out, int threads);
 
 } // namespace lfm

@@ -449,3 +449,31 @@ def test_gpu_bunzip2_matches_libbz2(lfmlib, gpu):
     out, flags = lfmlib.bunzip2_device([bz2.compress(big, 1), bytes(bad)], 160000)
     assert flags[0] == 1 and out[0] is None
     assert flags[1] != 0 and out[1] is None
+
+
+def test_roi_read_small_blocks_gpu(lfmlib, oracle, gpu, tmp_path):
+    """ROI reads of predicted files with many blocks (only the blocks up / left
+    of the ROI decoded, on the GPU path) equal the crop of the image: every
+    family at predictor 4, and a tiles video stack (odd first frames)."""
+    import ctypes
+    rng = np.random.default_rng(11)
+    img = oracle.synthetic_lf(150, 110, Z=6, T=13, seed=0x4C464D07)[0, 0]
+    cases = [("tiles", 0), ("angle", 0), ("space", 0), ("tiles", 1)]
+    for fam, video in cases:
+        p = tmp_path / ("roi_%s_%d.lfm" % (fam, video))
+        lfmlib.write_lfm(str(p), img, predictor_request=8 + 4, nnum=13, video=video, block_size=[32, 24, 2, 1, 1],
+                         family=fam)
+        try:
+            for _ in range(6):
+                lb, ub = [], []
+                for d in (150, 110, 6, 1, 1):
+                    a, b = sorted(int(v) for v in rng.integers(0, d, size=2))
+                    lb.append(a)
+                    ub.append(b)
+                out = np.empty((ub[2] - lb[2] + 1, ub[1] - lb[1] + 1, ub[0] - lb[0] + 1), np.uint16)
+                rc = lfmlib.lib().readKLBroiInPlace(os.fsencode(str(p)), out.ctypes.data, (ctypes.c_uint32 * 5)(*lb),
+                                                     (ctypes.c_uint32 * 5)(*ub), 4)
+                assert rc == 0
+                assert np.array_equal(out, img[lb[2]:ub[2] + 1, lb[1]:ub[1] + 1, lb[0]:ub[0] + 1]), (fam, video, lb, ub)
+        finally:
+            lfmlib.set_family("tiles")

@@ -152,6 +152,65 @@ def test_roi_read(lfmlib, tmp_path):
     assert np.array_equal(out, img[3:10, 20:101, 10:61])
 
 
+def _read_roi(lfmlib, path, lb, ub, dtype=np.uint16):
+    import ctypes
+    shape = tuple(ub[d] - lb[d] + 1 for d in (4, 3, 2, 1, 0))
+    out = np.empty(shape, dtype)
+    rc = lfmlib.lib().readKLBroiInPlace(os.fsencode(str(path)), out.ctypes.data, (ctypes.c_uint32 * 5)(*lb),
+                                         (ctypes.c_uint32 * 5)(*ub), 2)
+    assert rc == 0, (lb, ub)
+    return out
+
+
+def _rois(dims, rng, n):
+    """ROIs over xyzct dims: the whole image, the last pixel, and n random boxes."""
+    yield [0] * 5, [d - 1 for d in dims]
+    yield [d - 1 for d in dims], [d - 1 for d in dims]
+    for _ in range(n):
+        lb, ub = [], []
+        for d in dims:
+            a, b = sorted(int(v) for v in rng.integers(0, d, size=2))
+            lb.append(a)
+            ub.append(b)
+        yield lb, ub
+
+
+def test_roi_reads_match_crop_of_full_decode(lfmlib, tmp_path):
+    """ROI reads decode only the blocks the ROI depends on (everything up / left
+    in its frames with predictors, the frame before an odd frame of a video
+    stack) and must equal the crop of the full image: predicted files of every
+    family, the video stack, and a 5-D raw file with border blocks on every axis."""
+    import lfm_oracle as O
+    man = _manifest()
+    rng = np.random.default_rng(7)
+    small = O.synthetic_lf(70, 45, Z=3, T=13, seed=0x4C464D06)
+    for fam in ("tiles", "angle", "space"):
+        lfmlib.set_family(fam)
+        try:
+            for k in (1, 4, 7):
+                p = os.path.join(GOLDEN, man["small_%s_req%d" % (fam, 8 + k)]["file"])
+                for lb, ub in _rois([70, 45, 3, 1, 1], rng, 4):
+                    got = _read_roi(lfmlib, p, lb, ub)
+                    want = small.reshape(1, 1, 3, 45, 70)[lb[4]:ub[4] + 1, lb[3]:ub[3] + 1, lb[2]:ub[2] + 1,
+                                                          lb[1]:ub[1] + 1, lb[0]:ub[0] + 1]
+                    assert np.array_equal(got, want), (fam, k, lb, ub)
+        finally:
+            lfmlib.set_family("tiles")
+    img = _img_tif()
+    p = os.path.join(GOLDEN, man["imgtif_stack_auto_video"]["file"])
+    Z, Y, X = img.shape
+    for lb, ub in _rois([X, Y, Z, 1, 1], rng, 6):
+        got = _read_roi(lfmlib, p, lb, ub)
+        assert np.array_equal(got[0, 0], img[lb[2]:ub[2] + 1, lb[1]:ub[1] + 1, lb[0]:ub[0] + 1]), (lb, ub)
+    img5 = O.synthetic_lf(37, 29, Z=5, C=2, Tn=3, T=7)
+    p5 = tmp_path / "r5.lfm"
+    lfmlib.write_lfm(p5, img5, predictor_request=8, nnum=7, block_size=[16, 8, 2, 1, 2])
+    for lb, ub in _rois([37, 29, 5, 2, 3], rng, 8):
+        got = _read_roi(lfmlib, p5, lb, ub)
+        want = img5[lb[4]:ub[4] + 1, lb[3]:ub[3] + 1, lb[2]:ub[2] + 1, lb[1]:ub[1] + 1, lb[0]:ub[0] + 1]
+        assert np.array_equal(got, want), (lb, ub)
+
+
 def test_invalid_predictor_request_rejected(lfmlib, tmp_path):
     img = np.zeros((1, 16, 16), np.uint16)
     with pytest.raises(lfmlib.LfmError, match="code 6"):
