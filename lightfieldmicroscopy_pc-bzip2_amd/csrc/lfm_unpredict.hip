@@ -19,6 +19,7 @@
 // so no barrier is needed; frames are independent (even frames first, then
 // odd temporal frames on their decoded predecessors).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include "lfm_cases.h"
@@ -293,6 +294,30 @@ __device__ __forceinline__ int inv_any3(NbVals& g, int tc, int uc, int res, int 
     return 0;
 }
 
+// the four position cases of tile case TC, evaluated branch-free and
+// selected per lane (u = x % T, v = y % T)
+template <int FAM, int K, int TC, bool TEMP>
+__device__ __forceinline__ int inv_tile3(NbVals& g, int res, int P, int u, int v)
+{
+    const int vc = inv_case3<FAM, K, TC, UC_COL, TEMP>(g, res, P);
+    const int vk = inv_case3<FAM, K, TC, UC_CORNER, TEMP>(g, res, P);
+    const int vr = inv_case3<FAM, K, TC, UC_ROW, TEMP>(g, res, P);
+    const int vi = inv_case3<FAM, K, TC, UC_IN, TEMP>(g, res, P);
+    return u == 0 ? (v > 0 ? vc : vk) : (v == 0 ? vr : vi);
+}
+
+// every tile case (edge steps: x < T in some lane, or the frame's first band)
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ int inv_edge3(NbVals& g, int res, int P, int u, int v, int tx, int ty, bool all_x)
+{
+    const int vxy = inv_tile3<FAM, K, TC_XY, TEMP>(g, res, P, u, v);
+    const int vx0 = inv_tile3<FAM, K, TC_X0, TEMP>(g, res, P, u, v);
+    if (all_x) return ty == 0 ? vx0 : vxy;  // no lane has x < T
+    const int v0y = inv_tile3<FAM, K, TC_0Y, TEMP>(g, res, P, u, v);
+    const int v00 = inv_tile3<FAM, K, TC_00, TEMP>(g, res, P, u, v);
+    return tx == 0 ? (ty == 0 ? v00 : v0y) : (ty == 0 ? vx0 : vxy);
+}
+
 template <int FAM, int K, bool TEMP>
 __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring, uint16_t* top)
 {
@@ -342,7 +367,7 @@ __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring,
         NbVals nf;
         nf.v[NB_A] = 0;
         load_far(nf, -r);
-        const int edge_k = y0 == 0 ? 1 << 30 : T + 63;  // steps before this run the case switch
+        const int edge_k = T + 63;  // before this step some lane has x < T
         for (int k0 = 0; k0 < W + 63; k0 += kSymAhead) {
 #pragma unroll
             for (int j = 0; j < kSymAhead; ++j) {
@@ -366,17 +391,8 @@ __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring,
                 const int res = unsymbolize16(sv);
                 const int P = TEMP ? (int)pv : 0;
                 int val;
-                if (k >= edge_k) {  // every valid lane: tile case XY
-                    const int vc = inv_case3<FAM, K, TC_XY, UC_COL, TEMP>(g, res, P);
-                    const int vk = inv_case3<FAM, K, TC_XY, UC_CORNER, TEMP>(g, res, P);
-                    const int vr = inv_case3<FAM, K, TC_XY, UC_ROW, TEMP>(g, res, P);
-                    const int vi = inv_case3<FAM, K, TC_XY, UC_IN, TEMP>(g, res, P);
-                    val = u == 0 ? (v > 0 ? vc : vk) : (v == 0 ? vr : vi);
-                } else {
-                    const int tc = tx == 0 ? (ty == 0 ? TC_00 : TC_0Y) : (ty == 0 ? TC_X0 : TC_XY);
-                    const int uc = u == 0 ? (v > 0 ? UC_COL : UC_CORNER) : (v == 0 ? UC_ROW : UC_IN);
-                    val = ok ? inv_any3<FAM, K, TEMP>(g, tc, uc, res, P) : 0;
-                }
+                if (k >= edge_k && y0 > 0) val = inv_tile3<FAM, K, TC_XY, TEMP>(g, res, P, u, v);
+                else val = inv_edge3<FAM, K, TEMP>(g, res, P, u, v, tx, ty, k >= edge_k);
                 const uint16_t o = (uint16_t)val;
                 if (ok) {
                     ring[r * kRing + (x & (kRing - 1))] = o;
@@ -392,6 +408,200 @@ __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring,
             }
         }
     }
+}
+
+// band4: band3 with the bands of a frame pipelined over NW waves of one
+// workgroup (wave w takes bands w, w + NW, ...).  Each wave publishes its
+// progress (band * stride + steps done) in LDS every kSync steps, after its
+// global stores have completed.  The rows a band needs from the band above
+// (its last T+1 rows) are read from the output in memory, a round of kSync
+// columns at a time, two rounds ahead of their use (workgroup-scope loads: the
+// waves share the CU's write-through L1), into a private LDS ring of kHand
+// columns: a
+// wave only ever waits for the band above to be far enough ahead, so the
+// waits form a chain from the first band down and cannot deadlock.
+constexpr int kHand = 128;
+constexpr int kSync = 32;
+
+template <int FAM, int K, bool TEMP>
+__device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv, uint16_t* lds, int ring_off,
+                                      int hand_off, int* pos)
+{
+    const int r = threadIdx.x & 63;
+    const size_t fs = (size_t)p.W * p.H;
+    const uint16_t* sym = p.sym + fz * fs;
+    uint16_t* out = p.out + fz * fs;
+    const uint16_t* prev = TEMP ? (fz ? p.out + (fz - 1) * fs : p.prev) : nullptr;
+    const int W = p.W, H = p.H, T = p.T, TT = T + 1;
+    const int nbands = (H + 63) / 64, kend = W + 63, stride = W + 64 + 3 * kSync;
+    const int prodw = (wv + NW - 1) % NW;
+    // (bounded: a broken hand-over shows up as wrong pixels, never as a hang)
+    auto wait_ge = [&](int need) {
+        for (int spin = 0; spin < (1 << 24) &&
+                           __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < need;
+             ++spin)
+            __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    // the band's stores are complete (in the CU's write-through L1 / the L2)
+    // before its progress is published
+    auto publish = [&](int v) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_s_waitcnt(0);
+        if (r == 0) __hip_atomic_store(pos + wv, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto far = [&](int x, int dx, int dy) -> int {
+        const int rr = r + dy;
+        return rr >= 0 ? ring_off + rr * kRing + ((x + dx) & (kRing - 1))
+                       : hand_off + (TT + rr) * kHand + ((x + dx) & (kHand - 1));
+    };
+    const int btop = hand_off + (TT - 1) * kHand;
+    // hand-over loader: lane l takes row l / 2 of the band above's last TT
+    // rows and 8 column pairs of a kSync-column round
+    const int hr = r >> 1, hc = (r & 1) * 16;
+    const bool hl = hr < TT;
+    uint32_t hv[8];
+    for (int b = wv; b < nbands; b += NW) {
+        const int y0 = b * 64;
+        const int y = y0 + r;
+        const bool row_ok = y < H;
+        const int v = y % T, ty = y / T;
+        const uint16_t* srow = sym + (size_t)(row_ok ? y : 0) * W;
+        const uint16_t* prow = TEMP ? prev + (size_t)(row_ok ? y : 0) * W : nullptr;
+        uint16_t* orow = out + (size_t)(row_ok ? y : 0) * W;
+        const uint32_t* hsrc = (const uint32_t*)(out + (size_t)(b > 0 && hl ? y0 - TT + hr : 0) * W);
+        auto hload = [&](int c0) {  // columns c0 + hc .. + 16 of the round starting at column c0
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int c = min(c0 + hc + 2 * q, W - 2);
+                hv[q] = __hip_atomic_load(hsrc + (c >> 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        };
+        auto hstore = [&](int c0) {
+            if (hl) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    *(uint32_t*)(lds + hand_off + hr * kHand + ((c0 + hc + 2 * q) & (kHand - 1))) = hv[q];
+            }
+        };
+        // symbols (and previous-frame pixels) in aligned groups of 8 columns:
+        // the current group and the next, loaded 8 columns before its use
+        // (one 16-byte load per lane every 8 steps instead of 8 2-byte loads:
+        // each load instruction touches one line per active lane)
+        // symbols (and previous-frame pixels) in aligned groups of 8 columns:
+        // the current group and the next, loaded 8 columns before its use
+        // (one 16-byte load per lane every 8 steps instead of 8 2-byte loads:
+        // each load instruction touches one line per active lane)
+        const int ng = W / 8;
+        uint4 scur = *(const uint4*)srow, snxt = *(const uint4*)(srow + 8 * min(1, ng - 1));
+        uint4 pcur{}, pnxt{};
+        if (TEMP) {
+            pcur = *(const uint4*)prow;
+            pnxt = *(const uint4*)(prow + 8 * min(1, ng - 1));
+        }
+        uint32_t ob0 = 0, ob1 = 0, ob2 = 0, ob3 = 0;  // the output group being filled
+        int u = 0, tx = 0;
+        int p1 = 0, p2 = 0;
+        auto load_far = [&](NbVals& f, int x) {
+            f.v[NB_B] = r == 0 && x >= 0 ? (int)lds[btop + (x & (kHand - 1))] : 0;
+            f.v[NB_C] = r == 0 && x >= 1 ? (int)lds[btop + ((x - 1) & (kHand - 1))] : 0;
+            f.v[NB_AP] = lds[far(x, -T, 0)];
+            f.v[NB_BP] = lds[far(x, 0, -T)];
+            f.v[NB_CP] = lds[far(x, -T, -T)];
+            f.v[NB_AP1] = lds[far(x, -TT, 0)];
+            f.v[NB_BP1] = lds[far(x, 0, -TT)];
+            f.v[NB_ABP] = lds[far(x, -1, -T)];
+            f.v[NB_BAP] = lds[far(x, -T, -1)];
+        };
+        if (b > 0) {  // the first two rounds' columns of the band above
+            wait_ge((b - 1) * stride + min(2 * kSync + 72, kend));
+            hload(0);
+            hstore(0);
+            hload(kSync);
+            hstore(kSync);
+        }
+        NbVals nf;
+        nf.v[NB_A] = 0;
+        load_far(nf, -r);
+        const int edge_k = T + 63;  // before this step some lane has x < T
+        for (int k0 = 0; k0 < kend; k0 += kSymAhead) {
+            if ((k0 & (kSync - 1)) == 0) {
+                publish(b * stride + k0);
+                if (b > 0) {
+                    if (k0 > 0) hstore(k0 + kSync);  // loaded last round
+                    wait_ge((b - 1) * stride + min(k0 + 3 * kSync + 72, kend));
+                    hload(k0 + 2 * kSync);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kSymAhead; ++j) {
+                const int k = k0 + j;
+                const int x = k - r;
+                const int xs = x & 7;
+                auto pick = [&](const uint4& q) {  // column xs of the group (two 64-bit halves
+                    // and a shift: a select chain here became a dynamically indexed stack copy)
+                    const uint64_t a = ((uint64_t)q.y << 32) | q.x, c = ((uint64_t)q.w << 32) | q.z;
+                    return (uint32_t)(((xs & 4) ? c : a) >> (16 * (xs & 3))) & 0xFFFFu;
+                };
+                const uint32_t sv = pick(scur), pv = TEMP ? pick(pcur) : 0u;
+                const bool ok = row_ok && x >= 0 && x < W;
+                NbVals g = nf;
+                load_far(nf, x + 1);
+                g.v[NB_A] = p1;
+                g.v[NB_B] = __builtin_amdgcn_update_dpp(g.v[NB_B], p1, 0x138, 0xF, 0xF, false);
+                g.v[NB_C] = __builtin_amdgcn_update_dpp(g.v[NB_C], p2, 0x138, 0xF, 0xF, false);
+                const int res = unsymbolize16(sv);
+                const int P = TEMP ? (int)pv : 0;
+                int val;
+                if (k >= edge_k && y0 > 0) val = inv_tile3<FAM, K, TC_XY, TEMP>(g, res, P, u, v);
+                else val = inv_edge3<FAM, K, TEMP>(g, res, P, u, v, tx, ty, k >= edge_k);
+                const uint16_t o = (uint16_t)val;
+                if (ok) {
+                    lds[ring_off + r * kRing + (x & (kRing - 1))] = o;
+                    const uint32_t ov = o;
+                    ob0 = xs == 0 ? ov : xs == 1 ? ob0 | ov << 16 : ob0;
+                    ob1 = xs == 2 ? ov : xs == 3 ? ob1 | ov << 16 : ob1;
+                    ob2 = xs == 4 ? ov : xs == 5 ? ob2 | ov << 16 : ob2;
+                    ob3 = xs == 6 ? ov : xs == 7 ? ob3 | ov << 16 : ob3;
+                    if (xs == 7) {  // the group is complete: one 16-byte store, next symbols
+                        *(uint4*)(orow + x - 7) = uint4{ob0, ob1, ob2, ob3};
+                        const int gn = min(x / 8 + 2, ng - 1);
+                        scur = snxt;
+                        snxt = *(const uint4*)(srow + 8 * gn);
+                        if (TEMP) {
+                            pcur = pnxt;
+                            pnxt = *(const uint4*)(prow + 8 * gn);
+                        }
+                    }
+                    if (++u == T) {
+                        u = 0;
+                        ++tx;
+                    }
+                }
+                p2 = p1;
+                p1 = (int)o;
+            }
+        }
+        publish(b * stride + kend);
+    }
+}
+
+template <int FAM, int K>
+__global__ __launch_bounds__(512) void unpredict_band4(UnFrames p, int NW)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds4[];
+    __shared__ int pos[8];  // progress of each wave (band * stride + steps done)
+    const int fz = p.first + (int)blockIdx.x * p.step;
+    if (fz >= p.nz) return;
+    const int wv = threadIdx.x >> 6, TT = p.T + 1;
+    if (threadIdx.x < (unsigned)NW) pos[threadIdx.x] = -1;
+    __syncthreads();
+    const int base = 0;
+    const int per = 64 * kRing + TT * kHand;
+    const int ring_off = base + wv * per, hand_off = ring_off + 64 * kRing;
+    if (p.video && ((p.z0 + fz) & 1)) band4<FAM, K, true>(p, fz, NW, wv, lds4, ring_off, hand_off, pos);
+    else band4<FAM, K, false>(p, fz, NW, wv, lds4, ring_off, hand_off, pos);
 }
 
 template <int FAM, int K>
@@ -425,9 +635,32 @@ static bool band2_ok(const UnFrames& p)
     return p.T <= 30 && band2_lds(p) <= 160 * 1024 && !std::getenv("LFM_UNPREDICT_V1");
 }
 
+// waves per frame for band4 (0: not applicable; rows are read and written in
+// aligned 8-column groups, so W is a multiple of 8)
+static int band4_waves(const UnFrames& p)
+{
+    if (p.T < 2 || p.T > 30 || (p.W & 7) || std::getenv("LFM_UNPREDICT_V3") ||
+        std::getenv("LFM_UNPREDICT_V2"))
+        return 0;
+    static const int cap = [] {
+        const char* e = std::getenv("LFM_UNPREDICT_NW");
+        return e ? std::max(2, std::min(8, std::atoi(e))) : 8;
+    }();
+    const int nw = std::min(cap, (p.H + 63) / 64);
+    return nw >= 2 ? nw : 0;
+}
+
 template <int FAM, int K_>
 static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
 {
+    if (const int nw = band4_waves(p)) {
+        const size_t lds = (size_t)nw * (64 * kRing + (p.T + 1) * kHand) * 2;
+        const void* fn4 = (const void*)unpredict_band4<FAM, K_>;
+        if (hipFuncSetAttribute(fn4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL((unpredict_band4<FAM, K_>), dim3(grid), dim3(64 * nw), lds, st, p, nw);
+        return hipGetLastError();
+    }
     const size_t lds = band2_lds(p);
     // band3 reads a step's far neighbours one step early: T >= 2
     static const bool v2_env = std::getenv("LFM_UNPREDICT_V2") != nullptr;

@@ -376,7 +376,8 @@ def test_gpu_bzip2_host_fallback_streams(lfmlib, oracle, gpu):
     assert b == oracle.encode(img, header_version=8, nnum=13, data_type=0, block_size=[95000, 1, 1, 1, 1])
 
 
-@pytest.mark.parametrize("W,H,T", [(200, 150, 13), (64, 70, 31), (45, 31, 5), (1, 1, 13), (300, 130, 15), (70, 90, 2), (33, 70, 1)])
+@pytest.mark.parametrize("W,H,T", [(200, 150, 13), (64, 70, 31), (45, 31, 5), (1, 1, 13), (300, 130, 15), (70, 90, 2),
+                                   (33, 70, 1), (96, 600, 7), (136, 200, 30), (256, 330, 15)])
 def test_unpredict_kernel_inverts_forward(lfmlib, oracle, gpu, W, H, T):
     """The GPU inverse returns the raw frames for every family and predictor
     (spatial), and for tiles video stacks (temporal odd frames); the oracle's
