@@ -331,9 +331,14 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         uint32_t g = 0, gleft = 0, tb = 0, selw = 0;
         uint32_t es = 0, rs = 0;  // pending RUNA/RUNB run: length, next digit
         const int kk0 = 1 - 4 * (int)lane;
-        while (true) {
+        // one exit, at the bottom: an error sets flag and the iteration runs on
+        // harmlessly (no write past cap), so the loop stays a simple loop (with
+        // an exit per error the compiler threaded a state code through every
+        // iteration)
+        uint32_t sym = 0;
+        do {
             if (gleft == 0) {  // next group of 50 symbols: its table
-                if (g >= nSel || br.over()) { flag = kHost; break; }
+                flag |= (g >= nSel || br.over()) ? kHost : 0u;
                 if ((g & 7) == 0) selw = U(sel[g >> 3]);
                 tb = ((selw >> (4 * (g & 7))) & 15u) << LB;
                 ++g;
@@ -341,7 +346,8 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             }
             --gleft;
             const uint32_t e = U(lut[tb + br.peek(LB)]);
-            uint32_t len = e >> 9, sym = (e & 511u) - 1u;
+            uint32_t len = e >> 9;
+            sym = (e & 511u) - 1u;
             if (e == 0) {  // longer than LB bits: bzip2's limit walk
                 const uint32_t t = tb >> LB;
                 uint32_t zn = LB + 1;
@@ -350,59 +356,71 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                     ++zn;
                     zvec = (int32_t)br.peek(zn);
                 }
-                if (zn > kMaxLen) { flag = kHost; break; }
-                const int idx = zvec - (int32_t)U((uint32_t)sbase[t][zn]);
-                if (idx < 0 || idx >= alphaSize) { flag = kHost; break; }
-                sym = U(sperm[t][idx]);
+                const int idx = zvec - (int32_t)U((uint32_t)sbase[t][min(zn, (uint32_t)kMaxLen)]);
+                if (zn > kMaxLen || idx < 0 || idx >= alphaSize) {
+                    flag = kHost;
+                    zn = 1;
+                    sym = EOB;
+                } else {
+                    sym = U(sperm[t][idx]);
+                }
                 len = zn;
             }
             br.skip(len);
             if (sym <= 1) {  // RUNA / RUNB: one digit of a run of the list front
                 es += (sym + 1) << rs;
-                if (++rs > 21) { flag = kHost; break; }
-                continue;
-            }
-            if (rs) {  // the run ends: es copies of the list front
-                if (nblock + es > cap) { flag = kHost; break; }
-                const uint32_t uc = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
-                nblock += es;
-                while (es) {
-                    if (op == 0 && es >= 64) {  // whole 64-byte pieces straight out
-                        const uint32_t whole = es & ~63u;
-                        const uint32_t at = nblock - es;
-                        for (uint32_t k = lane; k < whole; k += 64) ll[at + k] = (uint8_t)uc;
-                        es -= whole;
-                        continue;
+                flag |= ++rs > 21 ? kHost : 0u;
+            } else {
+                if (rs) {  // the run ends: es copies of the list front
+                    if (nblock + es > cap) flag = kHost;
+                    else {
+                        const uint32_t uc = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
+                        nblock += es;
+                        while (es) {
+                            if (op == 0 && es >= 64) {  // whole 64-byte pieces straight out
+                                const uint32_t whole = es & ~63u;
+                                const uint32_t at = nblock - es;
+                                for (uint32_t k = lane; k < whole; k += 64) ll[at + k] = (uint8_t)uc;
+                                es -= whole;
+                                continue;
+                            }
+                            const uint32_t take = min(es, 64u - op);
+                            obuf = lane - op < take ? uc : obuf;
+                            op += take;
+                            es -= take;
+                            if (op == 64) {
+                                ll[nblock - es - 64 + lane] = (uint8_t)obuf;
+                                op = 0;
+                            }
+                        }
                     }
-                    const uint32_t take = min(es, 64u - op);
-                    obuf = lane - op < take ? uc : obuf;
-                    op += take;
-                    es -= take;
-                    if (op == 64) {
-                        ll[nblock - es - 64 + lane] = (uint8_t)obuf;
-                        op = 0;
+                    es = 0;
+                    rs = 0;
+                }
+                if (sym != EOB) {
+                    if (nblock >= cap) flag = kHost;
+                    else {
+                        const uint32_t nn = sym - 1;
+                        const uint32_t v =
+                            ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)((nn >> 2) & 63u)) >> (8 * (nn & 3))) & 0xFFu;
+                        // move to front: entries 0 .. nn shift up by one, v goes to 0
+                        // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
+                        const uint32_t up =
+                            (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
+                        const uint32_t sh = (mtfw << 8) | (up >> 24);
+                        const int k = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
+                        const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+                        mtfw = (sh & msk) | (mtfw & ~msk);
+                        obuf = lane == op ? v : obuf;
+                        ++nblock;
+                        if (++op == 64) {
+                            ll[nblock - 64 + lane] = (uint8_t)obuf;
+                            op = 0;
+                        }
                     }
                 }
-                rs = 0;
             }
-            if (sym == EOB) break;
-            if (nblock >= cap) { flag = kHost; break; }
-            const uint32_t nn = sym - 1;
-            const uint32_t v = ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)(nn >> 2)) >> (8 * (nn & 3))) & 0xFFu;
-            // move to front: entries 0 .. nn shift up by one, v goes to 0
-            // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
-            const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
-            const uint32_t sh = (mtfw << 8) | (up >> 24);
-            const int k = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
-            const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
-            mtfw = (sh & msk) | (mtfw & ~msk);
-            obuf = lane == op ? v : obuf;
-            ++nblock;
-            if (++op == 64) {
-                ll[nblock - 64 + lane] = (uint8_t)obuf;
-                op = 0;
-            }
-        }
+        } while (!flag && sym != EOB);
         if (flag) break;
         if (lane < op) ll[nblock - op + lane] = (uint8_t)obuf;
         if (origPtr >= nblock || nblock == 0) { flag = kHost; break; }
