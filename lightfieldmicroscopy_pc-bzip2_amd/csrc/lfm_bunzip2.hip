@@ -143,8 +143,7 @@ struct WaveBits {
     uint32_t wi;         // next word to enter the bit window
     uint64_t win;        // 64 bits from the current word on
     uint32_t off;        // bits of win already consumed (< 32)
-    uint32_t used;       // bits consumed since the stream start
-    uint32_t total;      // bits in the stream
+    uint32_t total;      // bits in the stream, counted from the first word's first bit
     // raw (unswapped) load with a clamped index: no branch and no use of the
     // value next to the load, so the wait lands where the word is first needed
     __device__ __forceinline__ uint32_t raw(uint32_t i) const { return w[min(i, nw - 1)]; }
@@ -163,8 +162,7 @@ struct WaveBits {
         w = (const uint32_t*)payload + (byte0 >> 2);
         nw = (uint32_t)((byte1 - (byte0 & ~3ull) + 3) >> 2);
         off = (uint32_t)(byte0 & 3) * 8;
-        used = 0;
-        total = (uint32_t)(byte1 - byte0) * 8;
+        total = (uint32_t)(byte1 - byte0) * 8 + off;
         base = 0;
         vq = fix(raw(threadIdx.x), threadIdx.x);
         vn = raw(64 + threadIdx.x);
@@ -179,7 +177,6 @@ struct WaveBits {
     __device__ __forceinline__ void skip(uint32_t nb)  // nb <= 32
     {
         off += nb;
-        used += nb;
         if (off >= 32) {
             off -= 32;
             win = (win << 32) | next();
@@ -191,7 +188,8 @@ struct WaveBits {
         skip(nb);
         return v;
     }
-    __device__ __forceinline__ bool over() const { return used > total; }
+    // bits consumed past the stream's end (win holds words wi - 2 and wi - 1)
+    __device__ __forceinline__ bool over() const { return 32 * (wi - 2) + off > total; }
 };
 
 template <int LB>
@@ -411,7 +409,9 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                         const int k = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
                         const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
                         mtfw = (sh & msk) | (mtfw & ~msk);
-                        obuf = lane == op ? v : obuf;
+                        // obuf[lane op] = v (v and op are wave-uniform)
+                        // (lane select in m0: one SGPR read per VALU op on this chip)
+                        asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(obuf) : "s"(v), "s"(op) : "m0");
                         ++nblock;
                         if (++op == 64) {
                             ll[nblock - 64 + lane] = (uint8_t)obuf;
