@@ -20,6 +20,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <zlib.h>
@@ -1438,8 +1439,8 @@ int decode_roi(const uint8_t* payload, size_t len, const klb_image_header& h, co
         const uint64_t id = ids[i], sz = h.getBlockCompressedSizeBytes(id);
         std::memcpy(spay.data() + (sub.blockOffset[i] - sz), payload + h.getBlockOffset(id), sz);
     });
-    std::vector<uint8_t> simg(sub.getImageSizeBytes());
-    const int rc = decode_payload(spay.data(), spay.size(), sub, simg.data(), threads, family);
+    std::unique_ptr<uint8_t[]> simg(new uint8_t[sub.getImageSizeBytes()]);  // (no zero fill: every byte is decoded)
+    const int rc = decode_payload(spay.data(), spay.size(), sub, simg.get(), threads, family);
     if (rc) return rc;
     const size_t row = (size_t)(ub[0] - lb[0] + 1) * bpp;
     uint8_t* q = out;
@@ -1449,7 +1450,7 @@ int decode_roi(const uint8_t* payload, size_t len, const klb_image_header& h, co
                 for (uint64_t y = lb[1]; y <= ub[1]; ++y) {
                     const uint64_t e = (lb[0] - o[0]) +
                                        n[0] * ((y - o[1]) + n[1] * ((z - o[2]) + n[2] * ((c - o[3]) + n[3] * (t - o[4]))));
-                    std::memcpy(q, simg.data() + e * bpp, row);
+                    std::memcpy(q, simg.get() + e * bpp, row);
                     q += row;
                 }
     return 0;
