@@ -419,6 +419,38 @@ def test_decode_roundtrip_through_gpu(lfmlib, oracle, gpu, tmp_path):
 
 
 @pytest.mark.gpu
+def test_decode_roundtrip_5d_through_gpu(lfmlib, oracle, gpu, tmp_path):
+    """5-D stacks (c, t > 1: one predictor volume per (c, t)) with small blocks
+    round-trip through the GPU writer and reader (pipelined inverse predictor,
+    W % 8 == 0), and ROI reads across c and t equal crops."""
+    import ctypes
+    img = oracle.synthetic_lf(256, 130, Z=4, C=2, Tn=3, T=13, seed=91)
+    rng = np.random.default_rng(5)
+    for fam, hv in (("tiles", 0x80 + 8 + 4), ("angle", 8 + 3)):
+        lfmlib.set_family(fam)
+        try:
+            p = tmp_path / ("rt5_%s.lfm" % fam)
+            lfmlib.write_lfm(str(p), img, predictor_request=hv & 0x7F, nnum=13, video=hv >> 7,
+                             block_size=[64, 32, 2, 1, 1])
+            out, _, _ = lfmlib.read_lfm(str(p))
+            assert np.array_equal(out, img), fam
+            for _ in range(4):
+                lb, ub = [], []
+                for d in (256, 130, 4, 2, 3):
+                    a, b = sorted(int(v) for v in rng.integers(0, d, size=2))
+                    lb.append(a)
+                    ub.append(b)
+                roi = np.empty(tuple(ub[d] - lb[d] + 1 for d in (4, 3, 2, 1, 0)), np.uint16)
+                rc = lfmlib.lib().readKLBroiInPlace(os.fsencode(str(p)), roi.ctypes.data, (ctypes.c_uint32 * 5)(*lb),
+                                                     (ctypes.c_uint32 * 5)(*ub), 4)
+                assert rc == 0
+                want = img[lb[4]:ub[4] + 1, lb[3]:ub[3] + 1, lb[2]:ub[2] + 1, lb[1]:ub[1] + 1, lb[0]:ub[0] + 1]
+                assert np.array_equal(roi, want), (fam, lb, ub)
+        finally:
+            lfmlib.set_family("tiles")
+
+
+@pytest.mark.gpu
 def test_gpu_bunzip2_matches_libbz2(lfmlib, gpu):
     """GPU bzip2 decoder against the system libbz2 (Python's bz2,
     the same format as the reference's vendored 1.0.6): streams of every level,
