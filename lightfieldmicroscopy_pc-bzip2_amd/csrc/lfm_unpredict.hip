@@ -263,7 +263,7 @@ __device__ __forceinline__ void band2(const UnFrames& p, int fz, uint16_t* ring,
 // before the step's own writes.  Outside the first band and the first T + 63
 // steps of a band every lane is in the interior tile case, so the four
 // position-case formulas are all evaluated and one is selected per lane (no
-// divergent case switch); the edge steps run the per-lane switch.
+// divergent case switch); edge steps evaluate all sixteen cases and select.
 struct NbVals {
     int v[NB_COUNT];
     template <int N>
@@ -278,20 +278,6 @@ __device__ __forceinline__ int inv_case3(NbVals& g, int r, int P)
     if constexpr (!TEMP) return r + pr;
     else if constexpr (F == F_Z) return r + P;
     else return r + ((pr + P) >> 1);
-}
-
-template <int FAM, int K, bool TEMP>
-__device__ __forceinline__ int inv_any3(NbVals& g, int tc, int uc, int res, int P)
-{
-    switch (tc * 4 + uc) {
-#define LFM_INV(TC_, UC_) case TC_ * 4 + UC_: return inv_case3<FAM, K, TC_, UC_, TEMP>(g, res, P);
-    LFM_INV(0, 0) LFM_INV(0, 1) LFM_INV(0, 2) LFM_INV(0, 3)
-    LFM_INV(1, 0) LFM_INV(1, 1) LFM_INV(1, 2) LFM_INV(1, 3)
-    LFM_INV(2, 0) LFM_INV(2, 1) LFM_INV(2, 2) LFM_INV(2, 3)
-    LFM_INV(3, 0) LFM_INV(3, 1) LFM_INV(3, 2) LFM_INV(3, 3)
-#undef LFM_INV
-    }
-    return 0;
 }
 
 // the four position cases of tile case TC, evaluated branch-free and
