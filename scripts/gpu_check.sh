@@ -18,7 +18,7 @@ step() {  # name timeout cmd...
     return $rc
 }
 rocm-smi --showproductname > "$OUT/rocm_smi.log" 2>&1 || true
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
 step smoke 300 python __graft_entry__.py smoke
 step bench 600 python bench.py --steps ${BENCH_STEPS:-2} --warmup 1
 if [ "${PROFILE:-1}" = "1" ]; then
