@@ -634,20 +634,51 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         L.b[cls][cbase[cls] + slot] = o + cb;
         L.e[cls][cbase[cls] + slot] = o + ce;
     }
-    // scatter: key = 8-byte prefix (big endian), value = start | preceding byte << 24
+    // scatter of the values only (start | preceding byte << 24): the sorters
+    // rebuild the 8-byte keys from the text (rot_key8_fast), which the L2s
+    // hold, instead of 8-byte scattered key writes and their re-read
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
         const uint32_t m = bucket_tile(T, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads) {
             const uint8_t* p = tile + 1 + k;
-            uint64_t key = 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) key = (key << 8) | p[q];
-            const uint32_t pos = atomicAdd(&hist[(uint32_t)(key >> 49)], 1u);
-            B.keys_a[o + pos] = key;
+            const uint32_t pos = atomicAdd(&hist[((uint32_t)p[0] << 7) | (p[1] >> 1)], 1u);
             B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
         }
         __syncthreads();
     }
+}
+
+// the first-round key of rotation i of a stream's text T (length n): its
+// 8-byte prefix, big endian.  Away from the wrap, three aligned dwords (the
+// stream's cap leaves >= 8 bytes after n) funnel-shifted; else byte by byte.
+__device__ __forceinline__ uint64_t rot_key8_fast(const uint8_t* __restrict__ T, uint32_t n, uint32_t i)
+{
+    if (i + 8 <= n) {
+        const uint32_t* w = (const uint32_t*)(T + (i & ~3u));
+        const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+        const uint32_t sh = (i & 3u) * 8u;
+        const uint64_t x = (uint64_t)d0 | ((uint64_t)d1 << 32);
+        const uint64_t le = sh ? (x >> sh) | ((uint64_t)d2 << (64u - sh)) : x;
+        return __builtin_bswap64(le);
+    }
+    uint64_t k = 0;
+    uint32_t j = i;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        k = (k << 8) | T[j];
+        j = j + 1 == n ? 0u : j + 1;
+    }
+    return k;
+}
+
+// keys_a for the chunks the rocPRIM segmented sort takes (one workgroup per chunk)
+__global__ __launch_bounds__(256) void bwt_chunk_keys(Batch B, const uint32_t* __restrict__ cbp,
+                                                      const uint32_t* __restrict__ cep)
+{
+    const uint32_t cb = cbp[blockIdx.x], ce = cep[blockIdx.x];
+    const uint32_t s = cb / B.cap, n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
+    for (uint32_t j = cb + threadIdx.x; j < ce; j += 256) B.keys_a[j] = rot_key8_fast(T, n, B.vals_a[j] & kIdxMask);
 }
 
 // The chunk's keys / values are loaded striped (element q * TH + t: coalesced),
@@ -658,8 +689,13 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
 // consumers (tie groups) recompute them from the text (rot_key8).
 template <int TH, int IPT>
 __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __restrict__ cbp,
-                                                     const uint32_t* __restrict__ cep)
+                                                     const uint32_t* __restrict__ cep, uint32_t nch, uint32_t per)
 {
+    // per > 0: XCD-aware order (workgroup b runs on XCD b % 8; chunks
+    // x * per .. x * per + per - 1, consecutive and mostly of one stream, all
+    // go to XCD x, so a stream's text is pulled into one L2)
+    const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
+    if (c >= nch) return;
     static_assert(IPT == 2 || IPT == 4 || IPT == 8, "flags are packed 2, 4 or 8 per thread");
     using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
     using ExK = rocprim::block_exchange<uint64_t, TH, IPT>;
@@ -676,14 +712,20 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
         typename ExV::storage_type ev;
         Xch x;
     } sm;
-    const uint32_t cb = cbp[blockIdx.x], ce = cep[blockIdx.x], m = ce - cb, t = threadIdx.x;
+    const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
+    const uint32_t s = cb / B.cap, n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
     uint64_t k[IPT];
     uint32_t v[IPT];
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
         const uint32_t j = q * TH + t;
-        k[q] = j < m ? B.keys_a[cb + j] : ~0ull;
         v[q] = j < m ? B.vals_a[cb + j] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = q * TH + t;
+        k[q] = j < m ? rot_key8_fast(T, n, v[q] & kIdxMask) : ~0ull;
     }
     // the sort's valid-item count refers to the blocked arrangement
     ExK().striped_to_blocked(k, k, sm.ek);
@@ -2363,21 +2405,32 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             hipStreamSynchronize(st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         static const int cs_shape = std::getenv("LFM_CS_SHAPE") ? std::atoi(std::getenv("LFM_CS_SHAPE")) : 0;
+        static const int cs_xcd = std::getenv("LFM_CS_XCD") ? std::atoi(std::getenv("LFM_CS_XCD")) : 1;
+        // grid and chunks-per-XCD of a chunk list (XCD-aware order unless LFM_CS_XCD=0)
+        auto cs_grid = [&](uint32_t nc, uint32_t& per) {
+            per = cs_xcd ? (nc + 7) / 8 : 0u;
+            return dim3(cs_xcd ? 8 * per : nc);
+        };
+        uint32_t per = 0;
         if (nch[0]) {
+            const dim3 g = cs_grid(nch[0], per);
             if (cs_shape == 1)  // 1024 threads x 2 items (same capacity)
-                hipLaunchKernelGGL((bwt_chunk_sort<2 * kCsThreads, kCsItems / 2>), dim3(nch[0]), dim3(2 * kCsThreads), 0,
-                                   st, B, CL.b[0], CL.e[0]);
+                hipLaunchKernelGGL((bwt_chunk_sort<2 * kCsThreads, kCsItems / 2>), g, dim3(2 * kCsThreads), 0, st, B,
+                                   CL.b[0], CL.e[0], nch[0], per);
             else if (cs_shape == 2)  // 256 threads x 8 items
-                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads / 2, kCsItems * 2>), dim3(nch[0]), dim3(kCsThreads / 2), 0,
-                                   st, B, CL.b[0], CL.e[0]);
+                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads / 2, kCsItems * 2>), g, dim3(kCsThreads / 2), 0, st, B,
+                                   CL.b[0], CL.e[0], nch[0], per);
             else
-                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), dim3(nch[0]), dim3(kCsThreads), 0, st, B,
-                                   CL.b[0], CL.e[0]);
+                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), g, dim3(kCsThreads), 0, st, B, CL.b[0],
+                                   CL.e[0], nch[0], per);
         }
-        if (nch[1])
-            hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), dim3(nch[1]), dim3(kBigThreads), 0, st, B,
-                               CL.b[1], CL.e[1]);
+        if (nch[1]) {
+            const dim3 g = cs_grid(nch[1], per);
+            hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
+                               CL.e[1], nch[1], per);
+        }
         if (nch[2]) {
+            hipLaunchKernelGGL(bwt_chunk_keys, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
             e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
                                                     nch[2], CL.b[2], CL.e[2], 0, 64 - kBucketBits, st);
             if (e == hipSuccess)
