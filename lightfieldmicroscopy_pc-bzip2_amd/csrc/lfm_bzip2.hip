@@ -472,8 +472,8 @@ constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 %
 
 // First round: every rotation by its 8-byte prefix, in two steps.
 //  bwt_bucket      one workgroup per stream: a counting sort of the rotations
-//                  by their leading 15 bits (byte 0, top 7 bits of byte 1), the
-//                  histogram in LDS; keys = the 8-byte prefix (big endian).
+//                  by their leading kBucketBits bits (byte 0, top bits of byte 1), the
+//                  histogram in LDS; only the values are scattered (the sorters rebuild the 8-byte big-endian keys from the text).
 //                  The stream's slot range is cut at bucket ends into chunks
 //                  of < 2 kChunk rotations (a cut after the bucket that holds
 //                  each multiple of kChunk; a bucket larger than kChunk is a
@@ -487,8 +487,10 @@ constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 %
 // previous device-wide 60-bit radix sort made 8 HBM passes.  Chunks above the
 // large sorter's capacity (one bucket of > kBigCap equal-prefix rotations) go
 // to a rocPRIM segmented sort.
-constexpr uint32_t kBucketBits = 15;
-constexpr uint32_t kBuckets = 1u << kBucketBits;
+constexpr uint32_t kBucketBits = 14;               // default: 64 KiB histogram, two workgroups per CU (LFM_BKT_BITS 13..15;
+                                                   // 15 bits / one workgroup per CU measured 3 % slower end to end,
+                                                   // 13 bits 18 % slower: more buckets overflow the small sorter)
+constexpr uint32_t kMinBucketBits = 13, kMaxBucketBits = 15;
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
 constexpr uint32_t kChunk = 1024;
@@ -529,9 +531,11 @@ __device__ __forceinline__ uint32_t bucket_tile(const uint8_t* __restrict__ T, u
     return m;
 }
 
+template <uint32_t BITS>
 __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists L)
 {
-    __shared__ uint32_t hist[kBuckets];  // 128 KiB
+    constexpr uint32_t kBuckets = 1u << BITS;
+    __shared__ uint32_t hist[kBuckets];  // 128 KiB at 15 bits
     __shared__ uint8_t tile[kBktTile + 16];
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
@@ -546,11 +550,11 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
     for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
     if (t < 3) ccount[t] = 0;
-    // histogram of the 15-bit bucket
+    // histogram of the BITS-bit bucket
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
         const uint32_t m = bucket_tile(T, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads)
-            atomicAdd(&hist[((uint32_t)tile[1 + k] << 7) | (tile[2 + k] >> 1)], 1u);
+            atomicAdd(&hist[((uint32_t)tile[1 + k] << (BITS - 8)) | (tile[2 + k] >> (16 - BITS))], 1u);
         __syncthreads();
     }
     // exclusive scan of the buckets; chunk cuts at bucket ends
@@ -641,7 +645,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         const uint32_t m = bucket_tile(T, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads) {
             const uint8_t* p = tile + 1 + k;
-            const uint32_t pos = atomicAdd(&hist[((uint32_t)p[0] << 7) | (p[1] >> 1)], 1u);
+            const uint32_t pos = atomicAdd(&hist[((uint32_t)p[0] << (BITS - 8)) | (p[1] >> (16 - BITS))], 1u);
             B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
         }
         __syncthreads();
@@ -2257,9 +2261,11 @@ size_t prim_tmp_bytes(uint32_t count, uint32_t cap)
     uint8_t* f = nullptr;
     size_t tmp = 0, q = 0;
     const size_t max_seg = (size_t)count * (cap / kBigCap + 1);
-    (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, (unsigned)max_seg, v, v, 0,
-                                              64 - kBucketBits);
-    tmp = std::max(tmp, q);
+    for (uint32_t bits = kMinBucketBits; bits <= kMaxBucketBits; ++bits) {
+        (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, (unsigned)max_seg, v, v, 0,
+                                                  64 - bits);
+        tmp = std::max(tmp, q);
+    }
     (void)rocprim::radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, 0, 64);
     tmp = std::max(tmp, q);
 
@@ -2400,7 +2406,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
-        hipLaunchKernelGGL(bwt_bucket, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
+        static const uint32_t bkt_bits = [] {
+            const int b = std::getenv("LFM_BKT_BITS") ? std::atoi(std::getenv("LFM_BKT_BITS")) : 0;
+            return b >= (int)kMinBucketBits && b <= (int)kMaxBucketBits ? (uint32_t)b : kBucketBits;
+        }();
+        if (bkt_bits == 13) hipLaunchKernelGGL(bwt_bucket<13>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
+        else if (bkt_bits == 15) hipLaunchKernelGGL(bwt_bucket<15>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
+        else hipLaunchKernelGGL(bwt_bucket<14>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
         if (!ok() || hipMemcpyAsync(nch, d_cnt, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
@@ -2432,7 +2444,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         if (nch[2]) {
             hipLaunchKernelGGL(bwt_chunk_keys, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
             e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
-                                                    nch[2], CL.b[2], CL.e[2], 0, 64 - kBucketBits, st);
+                                                    nch[2], CL.b[2], CL.e[2], 0, 64 - bkt_bits, st);
             if (e == hipSuccess)
                 hipLaunchKernelGGL(bwt_chunk_flags, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
         }
