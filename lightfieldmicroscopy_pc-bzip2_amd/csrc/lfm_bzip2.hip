@@ -2438,8 +2438,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         if (nch[1]) {
             const dim3 g = cs_grid(nch[1], per);
-            hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
-                               CL.e[1], nch[1], per);
+            static const int big_shape = std::getenv("LFM_BIG_SHAPE") ? std::atoi(std::getenv("LFM_BIG_SHAPE")) : 0;
+            if (big_shape == 1)  // 1024 threads x 4 items (same capacity; measured equal to 512 x 8)
+                hipLaunchKernelGGL((bwt_chunk_sort<2 * kBigThreads, kBigItems / 2>), g, dim3(2 * kBigThreads), 0, st, B,
+                                   CL.b[1], CL.e[1], nch[1], per);
+            else
+                hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
+                                   CL.e[1], nch[1], per);
         }
         if (nch[2]) {
             hipLaunchKernelGGL(bwt_chunk_keys, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
