@@ -1654,6 +1654,70 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
     for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rf[i] = rfreq[i / kMaxAlpha][i % kMaxAlpha];
 }
 
+// huff_select with a group's 50 symbols loaded straight into registers (25
+// dword loads from its 100 bytes; a row is 16-byte aligned and 100 is a
+// multiple of 4): no LDS tile, so ~8 KiB of LDS per workgroup and more
+// workgroups per CU to hide the loads.  The last, partial group pads with
+// symbol kMaxAlpha, whose packed lengths are 0 and which is not counted.
+// Same selectors and frequencies as huff_select (LFM_HSEL=0 selects that one).
+__global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
+{
+    __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
+    __shared__ uint64_t lpack[kMaxAlpha + 1];
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t nMTF = B.nmtf[s], nSel = B.nsel[s];
+    const int nGroups = (int)B.ngroups[s];
+    const int alphaSize = (int)stream_nin(B, s) + 2;
+    const uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
+    const uint16_t* mtfv = B.mtfv + (size_t)s * (B.cap + 8);
+    uint8_t* sel = B.sel + (size_t)s * B.sel_cap;
+    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rfreq[i / kMaxAlpha][i % kMaxAlpha] = 0;
+    for (int v = t; v <= kMaxAlpha; v += kHuffThreads) {
+        uint64_t lp = 0;
+        if (v < alphaSize)
+            for (int q = 0; q < nGroups; ++q) lp |= (uint64_t)len[q * kMaxAlpha + v] << (10 * q);
+        lpack[v] = lp;
+    }
+    __syncthreads();
+    for (uint32_t g = t; g < nSel; g += kHuffThreads) {
+        const uint32_t gs = g * kGSize, cnt = min(nMTF - gs, (uint32_t)kGSize);
+        uint32_t w[kGSize / 2];
+        if (cnt == (uint32_t)kGSize) {
+            const uint32_t* p = (const uint32_t*)(mtfv + gs);
+#pragma unroll
+            for (int q = 0; q < kGSize / 2; ++q) w[q] = p[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < kGSize / 2; ++q) {
+                const uint32_t lo = 2u * q < cnt ? mtfv[gs + 2 * q] : (uint32_t)kMaxAlpha;
+                const uint32_t hi = 2u * q + 1 < cnt ? mtfv[gs + 2 * q + 1] : (uint32_t)kMaxAlpha;
+                w[q] = lo | (hi << 16);
+            }
+        }
+        // a group's cost under every table at once (10-bit fields, as huff_select)
+        uint64_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < kGSize / 2; ++q) acc += lpack[w[q] & 0xFFFFu] + lpack[w[q] >> 16];
+        int bt = -1;
+        uint32_t bc = 999999999u;
+        for (int q = 0; q < nGroups; ++q) {
+            const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
+            if (cq < bc) { bc = cq; bt = q; }
+        }
+        sel[g] = (uint8_t)bt;
+#pragma unroll
+        for (int q = 0; q < kGSize / 2; ++q) {
+            const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
+            if (lo != (uint32_t)kMaxAlpha) atomicAdd(&rfreq[bt][lo], 1u);
+            if (hi != (uint32_t)kMaxAlpha) atomicAdd(&rfreq[bt][hi], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* rf = B.rfreq + (size_t)s * kMaxGroups * kMaxAlpha;
+    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rf[i] = rfreq[i / kMaxAlpha][i % kMaxAlpha];
+}
+
 // BZ2_hbMakeCodeLengths for kLenTasks (stream, table) pairs per wave, one per
 // lane: the sequential heap code runs SIMT across tables instead of on one
 // lane.  Per-lane arrays are interleaved in LDS (element e of lane l at
@@ -2571,9 +2635,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             hipLaunchKernelGGL(mtf_win, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
         hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
     }
+    static const bool hsel = !(std::getenv("LFM_HSEL") && std::atoi(std::getenv("LFM_HSEL")) == 0);
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
     for (int it = 0; it < kIters; ++it) {
-        hipLaunchKernelGGL(huff_select, dim3(count), dim3(kHuffThreads), 0, st, B);
+        if (hsel) hipLaunchKernelGGL(huff_select_reg, dim3(count), dim3(kHuffThreads), 0, st, B);
+        else hipLaunchKernelGGL(huff_select, dim3(count), dim3(kHuffThreads), 0, st, B);
         static const int lanes = [] {
             const char* v = std::getenv("LFM_HUFF_LANES");
             const int x = v ? std::atoi(v) : kLenTasks;
