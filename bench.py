@@ -10,12 +10,23 @@ between steps.  After the timed steps (N=1) the last .lfm is decoded once
 (GPU bzip2 decode + GPU inverse predictor) and compared with the input: `decode`
 in the JSON line, for information (not the metric).
 
-Multi-GPU (torchrun, one process per GPU): rank r encodes z-slab r of a
-(world x 64)-frame stack (lfm.shard: slabs are whole blocks deep, so the slab
-files join byte-identically with lfm.merge_slabs, tests/test_shard_cpu.py);
-the predictor is selected on the stack's frame 0 redundantly on every rank
-(no broadcast) and forced for the slab; no data-path collective (scaling
-"weak"); a barrier + MAX-over-ranks of the timed region gives value.
+Multi-GPU (torchrun, one process per GPU): rank r encodes z-slab r (frames
+64r .. 64r+63) of a (world x 64)-frame stack; the predictor is selected on
+the stack's frame 0 redundantly on every rank (no broadcast) and forced for
+the slab.  Inside the timed region the ranks then build ONE .lfm of the whole
+stack in host shared memory: an all_gather of every slab's (payload bytes,
+block count) -- the path's only exchange, RCCL under nccl -- gives each rank
+its payload offset and first block index, and every rank places its own
+compressed blocks and offset-table entries there concurrently
+(lfm.place_slab; equal to lfm.merge_slabs).  Scaling "weak"; a barrier +
+MAX-over-ranks of the timed region gives value.
+
+After the timed steps the last .lfm is checked against the oracle's digests
+(tests/golden/full_size_manifest.json, reference bzip2-1.0.6): the whole-file
+SHA-256 of config 3 at N = 1, per-layer digests of the 512-frame stack at
+N > 1 (`verified` in the JSON line).  At N = 1 the same stack is also encoded
+from host memory (pinned and pageable), H2D inside the timed region:
+`host_input` (the PCIe-inclusive rate; `value` is always HBM-resident).
 
 Also reported: `roofline` of the dominant kernel (fused predictor, HIP-event
 time per launch on its own stream) and `cpu_baseline` = the reference's CPU
@@ -23,6 +34,7 @@ bzip2-only path (request 8, same blocks, the reference's own bzip2-1.0.6 from
 oracle/_ref) on a bounded sample, timed on this host.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -101,6 +113,104 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
             "value_1thread": px1 / dt1 / 1e6, "nproc": os.cpu_count()}
 
 
+def _manifest(name):
+    path = os.path.join(REPO, "tests", "golden", "full_size_manifest.json")
+    try:
+        return {e["name"]: e for e in json.load(open(path))}.get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def verify_lfm(buf, world, zf):
+    """Compare the timed .lfm with the oracle's digests (outside the timed region)."""
+    if world == 1 and zf == Z:
+        e = _manifest("cfg3_2048x2048x64_angle_auto")
+        if e is None:
+            return None
+        return {"against": "cfg3 whole-file SHA-256 (oracle, reference bzip2-1.0.6)",
+                "ok": hashlib.sha256(buf).hexdigest() == e["sha256"] and len(buf) == e["size"]}
+    e = _manifest("cfg3x8_2048x2048x512_angle_auto")
+    nlay = world * zf // 8
+    if e is None or zf % 8 or nlay > len(e["layer_sha256"]):
+        return None
+    per = e["nblocks"] // len(e["layer_sha256"])
+    nb = per * nlay
+    offs = np.frombuffer(buf, dtype="<u8", count=nb, offset=320)
+    base = 320 + 8 * nb
+    ok = int(np.frombuffer(buf, dtype="<u4", count=5, offset=2)[2]) == world * zf
+    prev = 0
+    for j in range(nlay):
+        end = int(offs[(j + 1) * per - 1])
+        ok = ok and hashlib.sha256(buf[base + prev:base + end]).hexdigest() == e["layer_sha256"][j]
+        prev = end
+    ok = ok and len(buf) == base + prev
+    if nlay == len(e["layer_sha256"]):
+        ok = ok and hashlib.sha256(buf).hexdigest() == e["sha256"]
+    return {"against": "%d layer SHA-256s of the %d-frame stack (oracle, reference bzip2-1.0.6)"
+                       % (nlay, len(e["layer_sha256"]) * 8), "ok": bool(ok)}
+
+
+class SharedLfm:
+    """The whole stack's .lfm in host shared memory, written by every rank."""
+
+    def __init__(self, rank, world, cap):
+        port = os.environ.get("MASTER_PORT", "0")
+        d = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+        self.path = os.path.join(d, "lfm_bench_%s_%d_%d.lfm" % (port, world, os.getuid()))
+        self.rank = rank
+        if rank == 0:
+            with open(self.path, "wb") as f:
+                f.truncate(cap)
+        dist.barrier()
+        self.buf = np.memmap(self.path, dtype=np.uint8, mode="r+", shape=(cap,))
+        self.len = 0
+
+    def close(self):
+        del self.buf
+        if self.rank == 0:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+
+
+def place_in_shared(shm, b, rank, world, total_z, backend, threads):
+    """all_gather of (payload bytes, blocks) per slab, then this rank's blocks
+    and offset-table entries into the shared .lfm (lfm.place_slab)."""
+    pb, nb = lfm.slab_info(b)
+    dev = "cuda" if backend == "nccl" else "cpu"
+    mine = torch.tensor([pb, nb], dtype=torch.int64, device=dev)
+    every = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    sizes = torch.stack(every).cpu().tolist()
+    payload_off = sum(x[0] for x in sizes[:rank])
+    block_idx = sum(x[1] for x in sizes[:rank])
+    total_blocks = sum(x[1] for x in sizes)
+    lfm.place_slab(b, shm.buf, total_z, total_blocks, block_idx, payload_off, threads)
+    shm.len = 320 + 8 * total_blocks + sum(x[0] for x in sizes)
+
+
+def host_input_rates(enc, d_img, zf, steps=2):
+    """PCIe-inclusive encode: the stack in host memory (pinned, then pageable),
+    uploaded by the encoder inside the timed region (selection included)."""
+    out = {}
+    h_pin = torch.empty(tuple(d_img.shape), dtype=torch.int16, pin_memory=True)
+    h_pin.copy_(d_img)
+    arrays = (("pinned", h_pin.numpy().view(np.uint16)), ("pageable", np.array(h_pin.numpy().view(np.uint16))))
+    for name, arr in arrays:
+        enc.encode(arr, header_version=0, nnum=T, copy=False)  # warm
+        t0 = time.perf_counter()
+        h2d = 0.0
+        for _ in range(steps):
+            _, st = enc.encode(arr, header_version=0, nnum=T, copy=False)
+            h2d += st["h2d_ms"]
+        dt = (time.perf_counter() - t0) / steps
+        out[name] = {"Mpixel_per_s": round(X * Y * zf / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 2),
+                     "h2d_ms": round(h2d / steps, 2)}
+    out["note"] = "host stack -> in-memory .lfm, H2D inside the timed region; value above is HBM-resident"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,6 +219,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--frames", type=int, default=Z)
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--no-host-input", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,7 +228,7 @@ def main():
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     # LFM_BENCH_BACKEND=gloo rehearses the N-rank path with several ranks on
     # one GPU (local rank modulo the visible devices); the driver's N-GPU runs
-    # use nccl (RCCL), which only carries the barriers and the MAX reduction
+    # use nccl (RCCL): the barriers, the slab-size all_gather and the MAX
     backend = os.environ.get("LFM_BENCH_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -132,16 +243,22 @@ def main():
     threads = host_threads(local_world)
 
     d_img = torch.empty((zf, Y, X), dtype=torch.int16, device="cuda")
-    # rank r holds z-slab r of a (world * zf)-frame stack
+    # rank r holds z-slab r (frames r*zf .. r*zf+zf-1) of a (world * zf)-frame stack
     z0 = rank * zf
-    lfm.synth_device(d_img, X, Y, zf, T, t_index=0, idx0=z0 * X * Y, seed=SEED)
+    lfm.synth_device(d_img, X, Y, zf, T, z0=z0, seed=SEED)
     if rank == 0:
         d_f0 = d_img[0]
     else:  # the stack's frame 0, for the redundant selection
         d_f0 = torch.empty((1, Y, X), dtype=torch.int16, device="cuda")
-        lfm.synth_device(d_f0, X, Y, 1, T, t_index=0, idx0=0, seed=SEED)
+        lfm.synth_device(d_f0, X, Y, 1, T, z0=0, seed=SEED)
     torch.cuda.synchronize()
     enc = lfm.Encoder(device=local, num_threads=threads)
+    shm = None
+    if world > 1:
+        nb_total = world * ((X + 95) // 96) * ((Y + 95) // 96) * ((zf + 7) // 8)
+        shm = SharedLfm(rank, world, 320 + 8 * nb_total + world * (X * Y * zf * 2 * 103 // 100 + (1 << 20)))
+
+    place_ms = []
 
     def step():
         t0 = time.perf_counter()
@@ -151,6 +268,10 @@ def main():
         b, st = enc.encode_slab(d_img, z0, header_version=forced_request(k), nnum=T, copy=False)
         st["select_ms"] = sel_ms
         st["total_ms"] += sel_ms
+        if shm is not None:
+            t1 = time.perf_counter()
+            place_in_shared(shm, b, rank, world, world * zf, backend, threads)
+            place_ms.append((time.perf_counter() - t1) * 1e3)
         return b, st
 
     for _ in range(args.warmup):
@@ -196,8 +317,11 @@ def main():
         "dtype": "u16",
         "data": "synthetic (SURVEY 8(d) integer light-field generator, generated on device)",
         "config": {"workload": "config 3: %dx%dx%d uint16 stack per GPU, Nnum %d, %s family, predictor auto-selected "
-                               "on frame 0, 96x96x8 blocks, bzip2, in-memory .lfm" % (X, Y, zf, T, FAMILY),
-                   "parallelism": "z-slab per GPU (no collective)", "host_threads_per_gpu": threads},
+                               "on frame 0, 96x96x8 blocks, bzip2, in-memory .lfm%s" % (
+                                   X, Y, zf, T, FAMILY,
+                                   "" if world == 1 else " of the whole %d-frame stack in host shared memory"
+                                   % (world * zf)),
+                   "parallelism": "z-slab per GPU (slab-size all_gather only)", "host_threads_per_gpu": threads},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "kernel": "lfm::predict_ring<1,K,4,1,3> (fused angle predictor + symbolize, %d frames per "
@@ -209,6 +333,17 @@ def main():
         "chosen_predictor": stats[-1]["chosen"],
         "ratio": round(px_rank * 2 / out_len, 4),
     }
+    if place_ms:
+        line["stages_ms"]["place_ms"] = round(float(np.mean(place_ms[-args.steps:])), 3)
+    # byte check of the last timed .lfm against the oracle (outside the timed region)
+    if rank == 0:
+        buf = b if shm is None else shm.buf[:shm.len]
+        line["verified"] = verify_lfm(buf, world, zf)
+        if world > 1:
+            line["ratio"] = round(world * px_rank * 2 / shm.len, 4)
+    if world > 1:
+        dist.barrier()
+        shm.close()
     if rank == 0 and world == 1 and not args.no_decode:
         buf = bytes(b)
         t1 = time.perf_counter()
@@ -218,8 +353,11 @@ def main():
         line["decode"] = {"ms": round(dms, 1), "Mpixel_per_s": round(px_rank / dms / 1e3, 1),
                           "exact": bool(np.array_equal(img.reshape(ref.shape), ref)),
                           "path": "GPU bzip2 decode + GPU inverse predictor (host libbz2 only for flagged streams, %d threads)" % threads}
+    if rank == 0 and world == 1 and not args.no_host_input:
+        line["host_input"] = host_input_rates(enc, d_img, zf)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)
+        line["cpu_baseline"]["affinity_cpus"] = len(os.sched_getaffinity(0))
     if rank == 0:
         print(json.dumps(line), flush=True)
     enc.close()

@@ -12,6 +12,7 @@
 #ifndef LFM_KLB_IMAGE_IO_H
 #define LFM_KLB_IMAGE_IO_H
 
+#include <atomic>
 #include <string>
 #include <cstdint>
 #include "klb_imageHeader.h"
@@ -44,6 +45,15 @@ public:
 
     int readImage(char* img, const klb_ROI* ROI, int numThreads);
     int readImageFull(char* img, int numThreads);
+
+    /* Selection helpers kept public as in the reference (src/klb_imageIO.h:91,101).
+     * Device pointers on the current HIP device.  bwt_entropy_2D: 2D entropy of
+     * header.getImageSizePixels() symbols (x0.96 into *entropy when is_src == 0;
+     * the unscaled value is returned).  predict_and_2DEntropy: candidates
+     * k = (*blockId)++ < numPredictors into out[k], scored into entropy[k]. */
+    float bwt_entropy_2D(uint16_t* In, float* entropy, int is_src);
+    int predict_and_2DEntropy(uint16_t* In, uint16_t** out, float* entropy, std::atomic<uint64_t>* blockId,
+                              int numPredictors);
 
 private:
     std::string filename;

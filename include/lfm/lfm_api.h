@@ -87,6 +87,39 @@ LFM_API int lfm_merge_slabs(const uint8_t* const* slabs, const uint64_t* lens, i
                             uint64_t* out_len);
 LFM_API void lfm_free(void* p);
 
+/* Multi-process writers (one process per GPU, e.g. torchrun): each rank
+ * places its own z-slab .lfm into the whole stack's .lfm buffer `dst`
+ * (shared memory), concurrently with the other ranks.  lfm_slab_info gives a
+ * slab's payload bytes and block count (the values the ranks exchange);
+ * lfm_place_slab copies the slab's payload to payload_offset (payload bytes
+ * of the slabs before it), writes its block end offsets re-based into the
+ * table at block_index (blocks before it) and, for block_index 0, the fixed
+ * header with the stack's depth total_z.  The result equals lfm_merge_slabs. */
+LFM_API int lfm_slab_info(const uint8_t* slab, uint64_t len, uint64_t* payload_bytes, uint64_t* nblocks);
+LFM_API int lfm_place_slab(const uint8_t* slab, uint64_t slab_len, uint8_t* dst, uint64_t dst_len, uint32_t total_z,
+                           uint64_t total_blocks, uint64_t block_index, uint64_t payload_offset, int numThreads);
+
+/* Devices the writers farm block ranges to (klb_imageIO::writeImage,
+ * writeKLBstack, writeLFMstack_c, lfm_encoder_encode_multi): n > 0 sets the
+ * list (a device may repeat: several workers on one GPU); n = 0 restores the
+ * default (env LFM_GPUS = "0,1,.." or a count, else every visible device).
+ * lfm_get_devices returns the count and fills up to cap entries. */
+LFM_API int lfm_set_devices(const int* devices, int n);
+LFM_API int lfm_get_devices(int* devices, int cap);
+
+/* Encode a HOST stack on the device list above (one host thread per device,
+ * block-layer ranges: z-slabs, or ranges of c / t), into the encoder's
+ * in-memory .lfm (byte-identical to a one-device encode).  Falls back to the
+ * encoder's own device when the list has one device or the stack one range. */
+LFM_API int lfm_encoder_encode_multi(lfm_encoder* enc, const void* img, const uint32_t xyzct[KLB_DATA_DIMS],
+                                     int dataType, int headerVersion, int Nnum,
+                                     const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                                     const char metadata[KLB_METADATA_SIZE], const uint8_t** out, uint64_t* out_len,
+                                     lfm_encode_stats* stats);
+
+/* Free the device / pinned buffers the writers keep between calls. */
+LFM_API void lfm_release_encoders(void);
+
 /* Decode an in-memory .lfm into `img` (host, getImageSizeBytes bytes). */
 LFM_API int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads);
 

@@ -102,9 +102,10 @@ int lfm_hip_scatter_blocks(const void* d_blocks, uint32_t stride, uint32_t first
                            const uint32_t dims[5], const uint32_t bs[5], uint32_t bpp, void* d_img, void* stream);
 
 /* Synthetic light-field stack of SURVEY.md 8(d) (integer generator) written
- * straight into device memory: X*Y*Z pixels of volume (c, t) = (0, t_index),
- * global pixel index offset idx0 (for z-slabs of a larger stack). */
-int lfm_hip_synth(uint16_t* d_out, int X, int Y, int Z, int T, int t_index, uint64_t idx0, uint64_t seed,
+ * straight into device memory: frames z0 .. z0+Z-1 (X*Y pixels each) of
+ * volume (c, t) = (0, t_index), global pixel index offset idx0 (a z-slab of a
+ * c = t = 1 stack: z0 = first frame, idx0 = z0*X*Y). */
+int lfm_hip_synth(uint16_t* d_out, int X, int Y, int Z, int T, int t_index, int z0, uint64_t idx0, uint64_t seed,
                   void* stream);
 
 /* number of visible HIP devices (0 when no GPU / no runtime) */

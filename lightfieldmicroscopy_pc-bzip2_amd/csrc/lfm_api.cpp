@@ -5,6 +5,8 @@
 #include <string>
 #include "klb_imageIO.h"
 #include "lfm_engine.h"
+#include "lfm_hip.h"
+#include <vector>
 
 struct lfm_encoder {
     lfm::Encoder enc;
@@ -90,6 +92,44 @@ extern "C" int lfm_encoder_encode_slab(lfm_encoder* e, const void* img, int img_
     return rc;
 }
 
+extern "C" int lfm_set_devices(const int* devices, int n)
+{
+    if (n < 0 || (n > 0 && !devices)) return 3;
+    std::vector<int> d(devices, devices + n);
+    const int count = lfm_hip_device_count();
+    for (int v : d)
+        if (v < 0 || v >= count) return 3;
+    lfm::set_encode_devices(d);
+    return 0;
+}
+
+extern "C" int lfm_get_devices(int* devices, int cap)
+{
+    const std::vector<int> d = lfm::encode_devices();
+    for (int i = 0; i < cap && i < (int)d.size(); ++i) devices[i] = d[i];
+    return (int)d.size();
+}
+
+extern "C" int lfm_encoder_encode_multi(lfm_encoder* e, const void* img, const uint32_t xyzct[KLB_DATA_DIMS],
+                                        int dataType, int headerVersion, int Nnum,
+                                        const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                                        const char metadata[KLB_METADATA_SIZE], const uint8_t** out,
+                                        uint64_t* out_len, lfm_encode_stats* stats)
+{
+    if (!e || !img || !out || !out_len) return 3;
+    klb_image_header h;
+    h.setHeader(xyzct, (KLB_DATA_TYPE)dataType, nullptr, blockSize, (KLB_COMPRESSION_TYPE)compressionType, metadata,
+                (uint8_t)headerVersion, (uint8_t)Nnum);
+    lfm::MemSink sink(&e->enc.mem_out);
+    int rc = lfm::encode_multi(img, h, sink, stats, e->threads, lfm::encode_devices());
+    if (rc == -1) rc = e->enc.encode(img, false, h, sink, stats, e->threads);
+    *out = e->enc.mem_out.data();
+    *out_len = e->enc.mem_out.size();
+    return rc;
+}
+
+extern "C" void lfm_release_encoders(void) { lfm::release_pooled_encoders(); }
+
 extern "C" int lfm_merge_slabs(const uint8_t* const* slabs, const uint64_t* lens, int nslabs, uint8_t** out,
                                uint64_t* out_len)
 {
@@ -107,6 +147,41 @@ extern "C" int lfm_merge_slabs(const uint8_t* const* slabs, const uint64_t* lens
 }
 
 extern "C" void lfm_free(void* p) { std::free(p); }
+
+extern "C" int lfm_slab_info(const uint8_t* slab, uint64_t len, uint64_t* payload_bytes, uint64_t* nblocks)
+{
+    klb_image_header h;
+    if (!slab || h.parseHeader(slab, len)) return 3;
+    const uint64_t body = h.Nb ? h.blockOffset[h.Nb - 1] : 0;
+    if (h.getSizeInBytes() + body > len) return 3;
+    if (payload_bytes) *payload_bytes = body;
+    if (nblocks) *nblocks = h.Nb;
+    return 0;
+}
+
+extern "C" int lfm_place_slab(const uint8_t* slab, uint64_t slab_len, uint8_t* dst, uint64_t dst_len,
+                              uint32_t total_z, uint64_t total_blocks, uint64_t block_index, uint64_t payload_offset,
+                              int numThreads)
+{
+    klb_image_header h;
+    if (!slab || !dst || h.parseHeader(slab, slab_len)) return 3;
+    if (h.xyzct[3] != 1 || h.xyzct[4] != 1 || block_index + h.Nb > total_blocks) return 3;
+    const uint64_t body = h.Nb ? h.blockOffset[h.Nb - 1] : 0;
+    const uint64_t hsz = 320 + 8 * total_blocks;
+    if (h.getSizeInBytes() + body > slab_len || hsz + payload_offset + body > dst_len) return 3;
+    if (block_index == 0) {  // the whole stack's fixed header (the offset table follows from every rank)
+        klb_image_header H(h);
+        H.xyzct[2] = total_z;
+        H.resizeBlockOffset(0);
+        if (H.calculateNumBlocks() != total_blocks) return 3;
+        H.serialize(dst, 320);
+    }
+    uint64_t* table = (uint64_t*)(dst + 320);  // little-endian host (x86-64)
+    for (size_t j = 0; j < h.Nb; ++j) table[block_index + j] = payload_offset + h.blockOffset[j];
+    lfm::par_memcpy(dst + hsz + payload_offset, slab + h.getSizeInBytes(), body,
+                    numThreads > 0 ? numThreads : lfm::default_threads());
+    return 0;
+}
 
 extern "C" int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads)
 {

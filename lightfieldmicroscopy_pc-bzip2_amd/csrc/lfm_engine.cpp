@@ -270,14 +270,19 @@ static int decompress_one(int ctype, const uint8_t* in, uint32_t n, uint8_t* out
     return 5;
 }
 
-int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads)
+int bzip2_level(const klb_image_header& h)
+{
+    return std::min(9, (int)((h.getBlockSizeBytes() + 99999) / 100000));  // klb_imageIO.cpp:108, nominal block
+}
+
+int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads, int level)
 {
     const BlockGrid g(h);
     const uint64_t nblocks = g.nblocks;
     h.resizeBlockOffset(nblocks);
     const size_t bpp = h.getBytesPerPixel();
     const uint32_t block_bytes = h.getBlockSizeBytes();                 // nominal (clamped) block
-    const int level = std::min(9, (int)((block_bytes + 99999) / 100000)); // klb_imageIO.cpp:108
+    if (level < 1) level = bzip2_level(h);
     uint32_t cap = block_bytes;
     if (h.compressionType != NONE) cap = (uint32_t)std::ceil((float)block_bytes * 2.0f + 50.0f);
     if (h.compressionType != NONE && h.compressionType != BZIP2 && h.compressionType != ZLIB) {
@@ -571,6 +576,14 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
     if (st) st->predict_ms += pred_ms_total;
     h.headerVersion = (uint8_t)((hv & 0x80) | k);
     if (st) st->chosen = k;
+    if (video && fam != 0 && k != 0 && Z > 1) {
+        // the reference writes these bytes (reproduced), but its temporal
+        // residual ((I - pred) + P) >> 1 drops a bit: no reader can restore
+        // the odd frames (lfm_Predictors_space.cu:114-177, _angle.cu:136-192)
+        std::fprintf(stderr, "WARNING: video stack with the %s predictor family: the odd frames are coded with the "
+                             "reference's lossy temporal residual and cannot be decoded exactly\n",
+                     fam == 1 ? "angle" : "space");
+    }
     if (keep) {
         *dsym = (const uint8_t*)d_sym_;
         return 0;
@@ -588,14 +601,14 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
 // GPU bzip2 of every block (lfm_bzip2.hip), streams batched to bound the
 // workspace; streams the device hands back (RLE1 block reaching nblockMAX,
 // periodic blocks) are compressed by libbz2 here.  Same bytes either way.
-int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st)
+int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level)
 {
     const BlockGrid g(h);
     const uint64_t nblocks = g.nblocks;
     h.resizeBlockOffset(nblocks);
     const size_t bpp = h.getBytesPerPixel();
     const uint32_t block_bytes = h.getBlockSizeBytes();
-    const int level = std::min(9, (int)((block_bytes + 99999) / 100000));  // klb_imageIO.cpp:108
+    if (level < 1) level = bzip2_level(h);
     const size_t out_cap = ((size_t)block_bytes + block_bytes / 50 + 4096 + 255) / 256 * 256;
     const size_t rle_cap = ((size_t)block_bytes + block_bytes / 4 + 64 + 255) / 256 * 256;
     // Batches run in a pipeline of kBzSlots HIP streams (one host thread
@@ -776,13 +789,8 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     return sink.finish(h);
 }
 
-int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
-                    const SlabSpec* slab)
+int normalize_header(klb_image_header& h)
 {
-    static const SlabSpec whole;
-    if (threads <= 0) threads = default_threads();
-    auto t0 = clk::now();
-    if (st) std::memset(st, 0, sizeof(*st));
     if (h.getBytesPerPixel() == 0) return 5;
     for (int d = 0; d < KLB_DATA_DIMS; ++d) {
         if (h.xyzct[d] == 0) return 3;
@@ -793,6 +801,40 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
         std::printf("ERROR: compression type %d not implemented\n", (int)h.compressionType);
         return 5;
     }
+    return 0;
+}
+
+int Encoder::select_host_frame(const void* frame, int W, int H, int T, int family, int* chosen, float entropy[8])
+{
+    if (int rc = ensure_gpu()) return rc;
+    (void)hipSetDevice(device_);
+    const size_t bytes = (size_t)W * H * 2;
+    if (!dev_alloc(d_in_, d_in_cap_, bytes)) return 3;
+    if (!dev_alloc(d_ws_, d_ws_cap_, lfm_hip_select_workspace_bytes(W, H))) return 3;
+    if (hipMemcpyAsync(d_in_, frame, bytes, hipMemcpyHostToDevice, stream_) != hipSuccess) return 3;
+    return lfm_hip_select((const uint16_t*)d_in_, W, H, T, family, entropy, chosen, d_ws_, stream_) == LFM_HIP_OK ? 0
+                                                                                                               : 3;
+}
+
+int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
+                    const SlabSpec* slab)
+{
+    static const SlabSpec whole;
+    if (threads <= 0) threads = default_threads();
+    auto t0 = clk::now();
+    if (st) std::memset(st, 0, sizeof(*st));
+    // a z-slab that starts past frame 0 lies in a stack at least one nominal
+    // block deeper than its start, so the stack's nominal block keeps the
+    // requested depth even where the slab's own last layer is shallower
+    int level = slab ? slab->level : -1;
+    if (level < 1 && slab && slab->z0 > 0 && h.getBytesPerPixel()) {
+        klb_image_header nominal(h);
+        for (int d = 0; d < KLB_DATA_DIMS; ++d)
+            if (d != 2 && nominal.blockSize[d]) nominal.blockSize[d] = std::min(nominal.blockSize[d], h.xyzct[d]);
+        if (nominal.blockSize[2] == 0) nominal.blockSize[2] = 1;
+        level = bzip2_level(nominal);
+    }
+    if (int rc = normalize_header(h)) return rc;
     const uint8_t* sym = nullptr;
     const uint8_t* dsym = nullptr;
     const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
@@ -801,9 +843,9 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
     auto tc = clk::now();
     if (gpu_bz) {
         if ((rc = ensure_gpu())) return rc;
-        rc = gpu_compress(dsym, h, sink, st);
+        rc = gpu_compress(dsym, h, sink, st, level);
     } else {
-        rc = compress_blocks(sym, h, sink, threads);
+        rc = compress_blocks(sym, h, sink, threads, level);
     }
     if (st) {
         st->compress_ms = ms_since(tc);
@@ -813,20 +855,6 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
         st->out_bytes = h.getCompressedFileSizeInBytes();
     }
     return rc;
-}
-
-Encoder& shared_encoder(std::unique_lock<std::mutex>& lock)
-{
-    static std::mutex mu;
-    static std::unique_ptr<Encoder> enc[64];
-    lock = std::unique_lock<std::mutex>(mu);
-    int dev = 0;
-    if (lfm_hip_device_count() > 0) {
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    }
-    dev = std::max(0, std::min(dev, 63));
-    if (!enc[dev]) enc[dev].reset(new Encoder(dev));
-    return *enc[dev];
 }
 
 // ------------------------------------------------------------ z-slab merge --
@@ -999,6 +1027,21 @@ struct Staging {
     hipEvent_t ev[2] = {nullptr, nullptr};
     bool used[2] = {false, false};
     int dev = -1;
+    Staging() = default;
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
+    ~Staging() { release(); }  // a worker thread that exits frees its pinned chunks
+    void release()
+    {
+        for (int i = 0; i < 2; ++i) {
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            if (buf[i]) (void)hipHostFree(buf[i]);
+            ev[i] = nullptr;
+            buf[i] = nullptr;
+            used[i] = false;
+        }
+        dev = -1;
+    }
     bool ready()
     {
         int d = 0;
@@ -1024,7 +1067,7 @@ Staging& staging()
     return s;
 }
 
-void par_memcpy(void* dst, const void* src, size_t n, int threads)
+void par_memcpy_impl(void* dst, const void* src, size_t n, int threads)
 {
     const size_t piece = 1u << 20;
     const uint64_t np = (n + piece - 1) / piece;
@@ -1051,7 +1094,7 @@ bool staged_h2d(void* d_dst, const void* h_src, size_t n, hipStream_t st, int th
         auto t0 = now();
         if (S.used[b] && hipEventSynchronize(S.ev[b]) != hipSuccess) return false;
         auto t1 = now();
-        par_memcpy(S.buf[b], (const uint8_t*)h_src + off, len, threads);
+        par_memcpy_impl(S.buf[b], (const uint8_t*)h_src + off, len, threads);
         auto t2 = now();
         t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
         t_copy += std::chrono::duration<double, std::milli>(t2 - t1).count();
@@ -1086,7 +1129,7 @@ bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int th
         const int b = (int)(i & 1);
         const size_t off = i * Staging::kChunk, len = std::min(Staging::kChunk, n - off);
         if (hipEventSynchronize(S.ev[b]) != hipSuccess) return false;
-        par_memcpy((uint8_t*)h_dst + off, S.buf[b], len, threads);
+        par_memcpy_impl((uint8_t*)h_dst + off, S.buf[b], len, threads);
         if (i + 2 < nc && !issue(i + 2)) return false;
     }
     return true;
@@ -1102,6 +1145,10 @@ struct DecodeBuffers {
     hipStream_t st = nullptr;
     void* p[N] = {};
     size_t cap[N] = {};
+    DecodeBuffers() = default;
+    DecodeBuffers(const DecodeBuffers&) = delete;
+    DecodeBuffers& operator=(const DecodeBuffers&) = delete;
+    ~DecodeBuffers() { release(); }  // a worker thread that exits frees its device buffers
     void release()
     {
         for (int i = 0; i < N; ++i) {
@@ -1150,6 +1197,8 @@ DecodeBuffers& decode_buffers()
 }
 } // namespace
 
+void par_memcpy(void* dst, const void* src, size_t n, int threads) { par_memcpy_impl(dst, src, n, threads); }
+
 // GPU decode of a BZIP2 payload (lfm_bunzip2.hip): payload up, streams decoded
 // in batches into the device image (the few flagged streams by the host
 // library), inverse predictor on the device, image down.  Returns -1 when the
@@ -1189,7 +1238,10 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     const size_t ws = lfm_hip_bunzip2_workspace_bytes((uint32_t)batch, block_bytes);
     static const bool keep = env_int("LFM_DECODE_KEEP", 1) != 0;
     auto release = [&]() {
-        if (!keep) DB.release();
+        if (!keep) {
+            DB.release();
+            staging().release();
+        }
     };
     void *d_pay = nullptr, *d_ws = nullptr, *d_blk = nullptr, *d_sym = nullptr, *d_out = nullptr;
     if (DB.begin()) {

@@ -92,15 +92,27 @@ private:
 // Compress every block of `sym` (image layout, bpp bytes per pixel) in
 // parallel and hand them to the sink in block order.  `h` must already hold
 // the clamped block size; its blockOffset table is filled.
-int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads);
+int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int threads, int level = -1);
 
 // z-slab [z0, z0 + xyzct[2]) of a larger stack (c = t = 1): the temporal
 // flag of frame z is video & (z0 + z), and the first frame's previous raw
 // frame is `prev` (host or device like the image) when z0 is odd.
+// level >= 1 overrides the bzip2 level rule (min(9, ceil(nominal block
+// bytes / 1e5)), klb_imageIO.cpp:108): a range of a larger stack codes at the
+// level of the whole stack's nominal block even when its own last block layer
+// is shallower.
 struct SlabSpec {
     uint32_t z0 = 0;
     const void* prev = nullptr;
+    int level = -1;
 };
+
+// clamp the block size to the dims and check the types (klb_imageIO.cpp:2402-2404)
+int normalize_header(klb_image_header& h);
+// bzip2 level of the reference's rule for the header's nominal block
+int bzip2_level(const klb_image_header& h);
+// multi-threaded memcpy (1 MiB pieces)
+void par_memcpy(void* dst, const void* src, size_t n, int threads);
 
 // Encoder: GPU predictor stage + block compression.  One per device; keeps
 // device / pinned buffers between calls.
@@ -113,11 +125,13 @@ public:
                const SlabSpec* slab = nullptr);
     PinnedBuffer mem_out;
     int device() const { return device_; }
+    // predictor selection on one host frame (uploaded to this encoder's device)
+    int select_host_frame(const void* frame, int W, int H, int T, int family, int* chosen, float entropy[8]);
 
 private:
     int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, const uint8_t** dsym,
                         lfm_encode_stats* st, const SlabSpec& slab);
-    int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st);
+    int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level);
     int ensure_gpu();
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     int device_;
@@ -140,8 +154,23 @@ private:
     void* h_sym_ = nullptr; size_t h_sym_cap_ = 0;   // pinned
 };
 
-// process-wide encoder for the C ABI / klb_imageIO (serialised by its mutex)
+// process-wide encoders for the C ABI / klb_imageIO, one per (device, worker
+// slot), kept between calls; `lock` holds the entry while it is used
 Encoder& shared_encoder(std::unique_lock<std::mutex>& lock);
+Encoder& pooled_encoder(int dev, int slot, std::unique_lock<std::mutex>& lock);
+void release_pooled_encoders();
+
+// devices the writer farms block ranges to: lfm_set_devices, else env
+// LFM_GPUS ("0,1,2" or a count), else every visible device
+std::vector<int> encode_devices();
+void set_encode_devices(const std::vector<int>& devs);
+
+// Multi-GPU writer (lfm_multigpu.cpp): host image, block-layer ranges farmed
+// to `devs` (one host thread each), selection once on frame 0, in-order
+// append to `sink`.  Returns -1 when the image does not split into two or
+// more ranges (the caller then encodes on one device).
+int encode_multi(const void* img, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
+                 const std::vector<int>& devs);
 
 // Assemble one .lfm from the .lfm files of consecutive z-slabs of a stack
 // (each encoded with the same forced predictor, slab i starting at the sum of

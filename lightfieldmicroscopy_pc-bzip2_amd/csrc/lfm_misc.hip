@@ -23,7 +23,7 @@ __device__ __forceinline__ int64_t tri(int64_t a)
 
 // v = 100 + lens*field/256 + noise  (<= 3235), one thread per 8 pixels (16-byte stores)
 __global__ __launch_bounds__(256) void synth_kernel(uint16_t* __restrict__ out, int X, int Y, int Z, int T, int t,
-                                                    uint64_t idx0, uint64_t seed)
+                                                    int z0, uint64_t idx0, uint64_t seed)
 {
     const uint64_t total = (uint64_t)X * Y * Z;
     const int64_t half = T / 2;
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void synth_kernel(uint16_t* __restrict__ out, 
             if (i >= total) { v[j] = 0; continue; }
             const int64_t x = (int64_t)(i % X);
             const int64_t y = (int64_t)((i / X) % Y);
-            const int64_t z = (int64_t)(i / ((uint64_t)X * Y));
+            const int64_t z = z0 + (int64_t)(i / ((uint64_t)X * Y));
             const int64_t du = (x % T) - half, dv = (y % T) - half;
             const int64_t lens = (1024 * (rm - (du * du + dv * dv))) / rm;
             const int64_t field = 256 + tri(3 * x + 40 * z + 97 * t) / 4 + tri(2 * y) / 4;
@@ -60,15 +60,15 @@ __global__ __launch_bounds__(256) void synth_kernel(uint16_t* __restrict__ out, 
 
 } // namespace lfm
 
-extern "C" int lfm_hip_synth(uint16_t* d_out, int X, int Y, int Z, int T, int t_index, uint64_t idx0, uint64_t seed,
+extern "C" int lfm_hip_synth(uint16_t* d_out, int X, int Y, int Z, int T, int t_index, int z0, uint64_t idx0, uint64_t seed,
                              void* stream)
 {
-    if (!d_out || X <= 0 || Y <= 0 || Z <= 0 || T <= 0) return LFM_HIP_EINVAL;
+    if (!d_out || X <= 0 || Y <= 0 || Z <= 0 || T <= 0 || z0 < 0) return LFM_HIP_EINVAL;
     const uint64_t total = (uint64_t)X * Y * Z;
     const uint64_t threads = (total + 7) / 8;
     const int grid = (int)(threads < 256ull * 2048 ? (threads + 255) / 256 : 2048);
     hipLaunchKernelGGL(lfm::synth_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, d_out, X, Y, Z, T, t_index,
-                       idx0, seed);
+                       z0, idx0, seed);
     return hipGetLastError() == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
 }
 

@@ -35,7 +35,8 @@ EXPORTS = [
     # lfm_api.h
     "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
-    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory",
+    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_set_devices", "lfm_get_devices",
+    "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab",
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
@@ -98,6 +99,17 @@ def lib():
                                           ctypes.c_int, ctypes.c_int, u32p, ctypes.c_int, ctypes.c_char_p,
                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
+    L.lfm_encoder_encode_multi.argtypes = [vp, vp, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p,
+                                           ctypes.c_int, ctypes.c_char_p,
+                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
+    L.lfm_slab_info.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.lfm_place_slab.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]
+    L.lfm_set_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.lfm_get_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.lfm_release_encoders.argtypes = []
+    L.lfm_release_encoders.restype = None
     L.lfm_merge_slabs.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
                                   ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_uint64)]
     L.lfm_free.argtypes = [vp]
@@ -123,7 +135,7 @@ def lib():
     L.lfm_hip_select.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, f32p,
                                  ctypes.POINTER(ctypes.c_int), vp, vp]
     L.lfm_hip_synth.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                ctypes.c_uint64, ctypes.c_uint64, vp]
+                                ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]
     _lib = L
     return L
 
@@ -140,6 +152,25 @@ def device_count():
 def require_gpu():
     if device_count() <= 0:
         raise LfmError("no HIP device visible: the LFM predictor stage runs only on the GPU")
+
+
+def set_devices(devices=None):
+    """Devices the writers farm block ranges to (lfm_set_devices); None or []
+    restores the default (env LFM_GPUS, else every visible device)."""
+    devices = list(devices or [])
+    arr = (ctypes.c_int * max(1, len(devices)))(*devices)
+    _check(lib().lfm_set_devices(arr, len(devices)), "lfm_set_devices")
+
+
+def get_devices():
+    arr = (ctypes.c_int * 256)()
+    n = lib().lfm_get_devices(arr, 256)
+    return list(arr[:min(n, 256)])
+
+
+def release_encoders():
+    """Free the device / pinned buffers the writers keep between calls."""
+    lib().lfm_release_encoders()
 
 
 def set_family(family):
@@ -235,6 +266,9 @@ class Encoder:
     """lfm_encoder: encode host arrays or device-resident tensors to .lfm bytes."""
 
     def __init__(self, device=-1, num_threads=-1):
+        if device < 0 and _HAVE_TORCH and torch.cuda.is_available():
+            device = torch.cuda.current_device()
+        self._device = device
         self._h = lib().lfm_encoder_create(device, num_threads)
         if not self._h:
             raise LfmError("lfm_encoder_create failed")
@@ -250,16 +284,30 @@ class Encoder:
         except Exception:
             pass
 
-    @staticmethod
-    def _operand(img, xyzct, data_type):
-        """(pointer, is_device, xyzct, data_type, keepalive) of a numpy array or torch tensor."""
+    _TORCH_KLB = {"torch.uint8": 0, "torch.uint16": 1, "torch.int16": 1, "torch.uint32": 2, "torch.uint64": 3,
+                  "torch.int8": 4, "torch.int32": 6, "torch.int64": 7, "torch.float32": 8, "torch.float64": 9}
+
+    def _operand(self, img, xyzct, data_type):
+        """(pointer, is_device, xyzct, data_type, keepalive) of a numpy array or torch tensor.
+        A CUDA tensor must be contiguous and live on this encoder's device;
+        int16 is taken as a uint16 view (torch has no uint16 arithmetic)."""
         if _HAVE_TORCH and isinstance(img, torch.Tensor):
             if img.is_cuda:
+                if not img.is_contiguous():
+                    raise LfmError("device input must be contiguous (got strides %s)" % (img.stride(),))
+                if self._device >= 0 and img.device.index != self._device:
+                    raise LfmError("device input lives on cuda:%d, the encoder on cuda:%d"
+                                   % (img.device.index, self._device))
+                kt = self._TORCH_KLB.get(str(img.dtype))
+                if kt is None:
+                    raise LfmError("unsupported tensor dtype %s" % img.dtype)
+                if data_type is not None and data_type != kt and not (data_type == 1 and kt in (1, 5)):
+                    raise LfmError("data_type %d does not match tensor dtype %s" % (data_type, img.dtype))
                 shape = list(img.shape)
                 while len(shape) < 5:
                     shape = [1] + shape
                 xyzct = xyzct or [shape[4], shape[3], shape[2], shape[1], shape[0]]
-                return img.data_ptr(), 1, xyzct, (1 if data_type is None else data_type), img
+                return img.data_ptr(), 1, xyzct, (kt if data_type is None else data_type), img
             img = img.numpy()
         img = np.ascontiguousarray(img)
         xyzct = xyzct or _xyzct(img)
@@ -280,6 +328,25 @@ class Encoder:
                                       _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
         _check(rc, "lfm_encoder_encode")
         del keep
+        if not copy:
+            return memoryview((ctypes.c_uint8 * n.value).from_address(ctypes.addressof(out.contents))), st.as_dict()
+        return ctypes.string_at(out, n.value), st.as_dict()
+
+    def encode_multi(self, img, header_version=0, nnum=13, block_size=None, compression=1, metadata=None,
+                     data_type=None, copy=True):
+        """Encode a HOST stack on every device of set_devices() (the multi-GPU
+        block scheduler behind klb_imageIO::writeImage).  Returns (.lfm, stats)."""
+        img = np.ascontiguousarray(img)
+        xyzct = _xyzct(img)
+        data_type = DTYPES[img.dtype] if data_type is None else data_type
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_uint64()
+        st = EncodeStats()
+        rc = lib().lfm_encoder_encode_multi(self._h, img.ctypes.data, _u32(xyzct), data_type, int(header_version),
+                                            int(nnum), _u32(block_size) if block_size is not None else None,
+                                            compression, _meta(metadata), ctypes.byref(out), ctypes.byref(n),
+                                            ctypes.byref(st))
+        _check(rc, "lfm_encoder_encode_multi")
         if not copy:
             return memoryview((ctypes.c_uint8 * n.value).from_address(ctypes.addressof(out.contents))), st.as_dict()
         return ctypes.string_at(out, n.value), st.as_dict()
@@ -322,6 +389,29 @@ def merge_slabs(slabs):
         return ctypes.string_at(out, ln.value)
     finally:
         lib().lfm_free(out)
+
+
+def _addr(buf):
+    """Address of a bytes / memoryview / numpy buffer (kept alive by the caller)."""
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    if isinstance(buf, bytes):
+        return ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+    return np.frombuffer(buf, dtype=np.uint8).ctypes.data
+
+
+def slab_info(slab):
+    """(payload bytes, block count) of a slab .lfm (what multi-process ranks exchange)."""
+    pb, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().lfm_slab_info(_addr(slab), len(slab), ctypes.byref(pb), ctypes.byref(nb)), "lfm_slab_info")
+    return pb.value, nb.value
+
+
+def place_slab(slab, dst, total_z, total_blocks, block_index, payload_offset, num_threads=-1):
+    """Place one rank's z-slab .lfm into the whole stack's .lfm buffer `dst`
+    (a writable numpy uint8 array, e.g. over shared memory) -- lfm_place_slab."""
+    _check(lib().lfm_place_slab(_addr(slab), len(slab), dst.ctypes.data, dst.nbytes, int(total_z), int(total_blocks),
+                                int(block_index), int(payload_offset), num_threads), "lfm_place_slab")
 
 
 def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):
@@ -432,5 +522,11 @@ def bunzip2_device(streams, out_stride, device="cuda", stream=None):
     return res, list(flags)
 
 
-def synth_device(d_out, X, Y, Z, T, t_index=0, idx0=0, seed=0x4C464D00, stream=None):
-    _check(lib().lfm_hip_synth(d_out.data_ptr(), X, Y, Z, T, t_index, idx0, seed, _stream(stream)), "lfm_hip_synth")
+def synth_device(d_out, X, Y, Z, T, t_index=0, idx0=None, seed=0x4C464D00, z0=0, stream=None):
+    """SURVEY 8(d) generator on the device: frames z0 .. z0+Z-1 of volume
+    (0, t_index); idx0 defaults to z0*X*Y (a z-slab of a c = t = 1 stack,
+    equal to oracle.synthetic_lf(..., z0=z0))."""
+    if idx0 is None:
+        idx0 = z0 * X * Y
+    _check(lib().lfm_hip_synth(d_out.data_ptr(), X, Y, Z, T, t_index, z0, idx0, seed, _stream(stream)),
+           "lfm_hip_synth")

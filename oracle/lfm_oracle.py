@@ -322,11 +322,15 @@ def splitmix64(x):
     return z ^ (z >> 31)
 
 
-def synthetic_lf(X, Y, Z=1, C=1, Tn=1, T=15, seed=0x4C464D00):
-    """SURVEY.md section 8(d) integer light-field generator (numpy restatement)."""
+def synthetic_lf(X, Y, Z=1, C=1, Tn=1, T=15, seed=0x4C464D00, z0=0):
+    """SURVEY.md section 8(d) integer light-field generator (numpy restatement).
+    z0 > 0 (C = Tn = 1): frames [z0, z0 + Z) of a taller stack, so large
+    stacks can be generated slab by slab."""
+    if z0:
+        assert C == 1 and Tn == 1
     x = np.arange(X, dtype=np.int64)[None, None, None, None, :]
     y = np.arange(Y, dtype=np.int64)[None, None, None, :, None]
-    z = np.arange(Z, dtype=np.int64)[None, None, :, None, None]
+    z = np.arange(z0, z0 + Z, dtype=np.int64)[None, None, :, None, None]
     t = np.arange(Tn, dtype=np.int64)[:, None, None, None, None]
     du = (x % T) - T // 2
     dv = (y % T) - T // 2
@@ -338,7 +342,7 @@ def synthetic_lf(X, Y, Z=1, C=1, Tn=1, T=15, seed=0x4C464D00):
         return np.abs((a % 2048) - 1024)
     field = 256 + tri(3 * x + 40 * z + 97 * t) // 4 + tri(2 * y) // 4
     shape = (Tn, C, Z, Y, X)
-    idx = np.arange(int(np.prod(shape)), dtype=np.uint64).reshape(shape)
+    idx = np.arange(z0 * Y * X, z0 * Y * X + int(np.prod(shape)), dtype=np.uint64).reshape(shape)
     noise = (_splitmix_vec(np.uint64(seed) ^ (idx * np.uint64(0x9E3779B97F4A7C15))) >> np.uint64(58)).astype(np.int64)
     v = 100 + (lens * field) // 256 + noise
     return np.broadcast_to(v, shape).astype(np.uint16)

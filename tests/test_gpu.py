@@ -15,6 +15,15 @@ pytestmark = pytest.mark.gpu
 FAMS = ["tiles", "angle", "space"]
 
 
+def ref_bz2(oracle, data, level):
+    """BZ2_bzBuffToBuffCompress(level, 0, 30) of the reference's own
+    bzip2-1.0.6, compiled from /root/reference by oracle/Makefile into
+    oracle/_ref/libbz2_ref.so (which travels to the GPU box)."""
+    bz = oracle.bzip2()
+    assert "reference" in bz.kind, "oracle/_ref/libbz2_ref.so missing: run make -C oracle"
+    return bz.compress(bytes(data), level)
+
+
 def dev16(torch, a):
     t = torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda()
     return t
@@ -144,7 +153,7 @@ def _gen(oracle, e):
     return eval("O." + e["generator"], {"O": oracle})
 
 
-@pytest.mark.parametrize("name", ["cfg2_512x512_space_auto", "cfg3s_512x512x8_angle_auto",
+@pytest.mark.parametrize("name", ["cfg1_imgtif_page0_req8", "cfg1_imgtif_stack_req8", "cfg2_512x512_space_auto", "cfg3s_512x512x8_angle_auto",
                                   "cfg4s_256x256x16_tiles_auto", "cfg5s_128x128x8x1x3_video_auto",
                                   "imgtif_page12_auto", "imgtif_stack_auto_video", "matlab_test_m"])
 def test_lfm_bytes_match_oracle_manifest(lfmlib, oracle, gpu, tmp_path, name):
@@ -212,8 +221,7 @@ def test_config3_full_size_properties(lfmlib, oracle, gpu):
 def test_full_size_encode_decode_roundtrip(lfmlib, oracle, gpu, fam):
     """2048 x 2048 x 64 through the whole GPU writer (selection, predictor,
     bzip2 batches) and back through the reader: every pixel returns, and a
-    sample of blocks equals libbzip2 byte for byte."""
-    import bz2
+    sample of blocks equals the reference's bzip2 byte for byte."""
     torch = gpu
     X, Y, Z, T = 2048, 2048, 64, 15
     d = torch.empty((Z, Y, X), dtype=torch.int16, device="cuda")
@@ -235,14 +243,13 @@ def test_full_size_encode_decode_roundtrip(lfmlib, oracle, gpu, fam):
         if coord[2] == 0 and bid % 17 == 0:
             blob = bytes(buf[h["header_size"] + prev:h["header_size"] + end])
             raw = oracle.gather_block(sym[None, None], coord, size)
-            assert blob == bz2.compress(raw, 2), bid
+            assert blob == ref_bz2(oracle, raw, 2), bid
         prev = end
 
 
-def test_gpu_bzip2_long_tied_list(lfmlib, gpu):
+def test_gpu_bzip2_long_tied_list(lfmlib, oracle, gpu):
     """More than 2^24 rotations tied after the first sort (binary alphabet):
     the tie rounds narrow their text keys so group index + text fit 64 bits."""
-    import bz2
     torch = gpu
     rng = np.random.default_rng(5)
     n, m = 140000, 125
@@ -251,7 +258,7 @@ def test_gpu_bzip2_long_tied_list(lfmlib, gpu):
     got, flags = lfmlib.bzip2_device(d, [n, m, 1, 1, 1], [n, 1, 1, 1, 1], 1, level=2)
     assert not any(flags)
     for i in range(0, m, 8):
-        assert got[i] == bz2.compress(data[i * n:(i + 1) * n].tobytes(), 2), i
+        assert got[i] == ref_bz2(oracle, data[i * n:(i + 1) * n].tobytes(), 2), i
 
 
 def test_synth_generator_matches_numpy(lfmlib, oracle, gpu):
@@ -322,18 +329,16 @@ def _bz2_cases():
     return cases
 
 
-def test_gpu_bzip2_matches_libbz2_edge_cases(lfmlib, gpu):
-    """Every GPU stream equals libbzip2 at the same level (python's bz2 is the
-    system libbz2 1.0.8, byte-identical to the reference's 1.0.6 on the KATs);
+def test_gpu_bzip2_matches_libbz2_edge_cases(lfmlib, oracle, gpu):
+    """Every GPU stream equals the reference's bzip2-1.0.6 at the same level;
     periodic blocks come back flagged for the host library."""
-    import bz2
     torch = gpu
     for name, data in _bz2_cases().items():
         n = len(data)
         d = torch.from_numpy(data.copy()).cuda()
         for level in (1, 2, 9):
             got, flags = lfmlib.bzip2_device(d, [n, 1, 1, 1, 1], [n, 1, 1, 1, 1], 1, level=level)
-            exp = bz2.compress(data.tobytes(), level)
+            exp = ref_bz2(oracle, data.tobytes(), level)
             if flags[0]:
                 assert name.startswith("periodic"), (name, level)
                 continue
@@ -343,8 +348,7 @@ def test_gpu_bzip2_matches_libbz2_edge_cases(lfmlib, gpu):
 
 def test_gpu_bzip2_block_grid_and_symbols(lfmlib, oracle, gpu):
     """Many streams from a 2-D block grid of predicted light-field symbols
-    (border blocks, uint16 samples) against libbzip2 per block."""
-    import bz2
+    (border blocks, uint16 samples) against the reference's bzip2 per block."""
     torch = gpu
     img = oracle.synthetic_lf(200, 150, Z=5, T=13, seed=21)[0, 0]
     sym = oracle.predict_volume(img, 13, "tiles", 4, 0)
@@ -355,7 +359,7 @@ def test_gpu_bzip2_block_grid_and_symbols(lfmlib, oracle, gpu):
     assert len(got) == len(blocks)
     for (i, coord, size), g in zip(blocks, got):
         raw = oracle.gather_block(sym[None, None], coord, size)
-        assert g == bz2.compress(raw, 1), i
+        assert g == ref_bz2(oracle, raw, 1), i
 
 
 def test_gpu_bzip2_host_fallback_streams(lfmlib, oracle, gpu):
@@ -451,12 +455,11 @@ def test_decode_roundtrip_5d_through_gpu(lfmlib, oracle, gpu, tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_bunzip2_matches_libbz2(lfmlib, gpu):
-    """GPU bzip2 decoder against the system libbz2 (Python's bz2,
-    the same format as the reference's vendored 1.0.6): streams of every level,
+def test_gpu_bunzip2_matches_libbz2(lfmlib, oracle, gpu):
+    """GPU bzip2 decoder on streams of the reference's bzip2-1.0.6:
+    streams of every level,
     long runs (RLE1 count bytes, RUNA/RUNB), random and periodic data, tiny
     blocks; a two-block stream and a damaged stream are flagged for the host."""
-    import bz2
     rng = np.random.default_rng(7)
     cases = []
     for level in (1, 2, 5, 9):
@@ -470,16 +473,16 @@ def test_gpu_bunzip2_matches_libbz2(lfmlib, gpu):
         (b"hello, light field", 9),
         (rng.integers(0, 2, 150000, dtype=np.uint8).repeat(3)[:147456].tobytes(), 2),
     ]
-    streams = [bz2.compress(d, lv) for d, lv in cases]
+    streams = [ref_bz2(oracle, d, lv) for d, lv in cases]
     out, flags = lfmlib.bunzip2_device(streams, 160000)
     for (d, lv), o, f in zip(cases, out, flags):
         assert f == 0, (lv, len(d), f)
         assert o == d, (lv, len(d))
     # two bzip2 blocks (more than 100k after RLE1 at level 1) -> host; a flipped bit -> not accepted
     big = rng.integers(0, 256, 150000, dtype=np.uint8).tobytes()
-    bad = bytearray(bz2.compress(b"some data to damage" * 100, 1))
+    bad = bytearray(ref_bz2(oracle, b"some data to damage" * 100, 1))
     bad[len(bad) // 2] ^= 0x10
-    out, flags = lfmlib.bunzip2_device([bz2.compress(big, 1), bytes(bad)], 160000)
+    out, flags = lfmlib.bunzip2_device([ref_bz2(oracle, big, 1), bytes(bad)], 160000)
     assert flags[0] == 1 and out[0] is None
     assert flags[1] != 0 and out[1] is None
 

@@ -1,8 +1,11 @@
 """Multi-GPU sharding of one stack on the CPU: the slab
 plan, the slab join (lfm_merge_slabs in liblfm, no GPU needed) against the
-oracle's one-piece encode, and the world-size-2 rank protocol over gloo
-(selection on the stack's frame 0 on every rank, one slab per rank, slabs
-gathered and joined on rank 0, MAX-over-ranks timing)."""
+oracle's one-piece encode, and the bench's world-size-2 rank protocol over
+gloo (selection on the stack's frame 0 on every rank, one slab per rank, an
+all_gather of slab sizes, every rank placing its blocks into one shared
+.lfm with lfm_place_slab, MAX-over-ranks timing).  The slabs here come from
+the oracle (no GPU); tests/test_multigpu_gpu.py runs the same protocol with
+the product encoder on the GPU."""
 import os
 import socket
 
@@ -77,14 +80,15 @@ def _rank_main(rank, world, port, result_path):
     import sys
     import torch.distributed as dist
     here = os.path.dirname(os.path.abspath(__file__))
-    for p in (os.path.join(os.path.dirname(here), "lightfieldmicroscopy_pc-bzip2_amd"),
-              os.path.join(os.path.dirname(here), "oracle")):
+    repo = os.path.dirname(here)
+    for p in (repo, os.path.join(repo, "lightfieldmicroscopy_pc-bzip2_amd"), os.path.join(repo, "oracle")):
         sys.path.insert(0, p)
-    import lfm
+    import bench
     import lfm_oracle as O
     from lfm.shard import forced_request, max_over_ranks, plan_slabs
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    shm = None
     try:
         Z, fam, bs = 24, "tiles", [32, 16, 8, 1, 1]
         img = O.synthetic_lf(64, 40, Z=Z, T=13, seed=0x4C464D04)  # every rank regenerates the stack (synthetic)
@@ -92,15 +96,19 @@ def _rank_main(rank, world, port, result_path):
         z0, d = plan_slabs(Z, world, 8)[rank]
         slab = O.encode(img[:, :, z0:z0 + d], header_version=forced_request(k, True), nnum=13, family=fam,
                         block_size=bs, z0=z0, prev=img[0, 0, z0 - 1] if z0 else None)
-        got = [None] * world
-        dist.all_gather_object(got, slab)
+        shm = bench.SharedLfm(rank, world, 1 << 22)
+        bench.place_in_shared(shm, slab, rank, world, Z, "gloo", 2)
+        dist.barrier()
         t = max_over_ranks(0.25 * (rank + 1))
         if rank == 0:
-            merged = lfm.merge_slabs(got)
+            merged = bytes(shm.buf[:shm.len])
             full = O.encode(img, header_version=0x80, nnum=13, family=fam, block_size=bs)
             with open(result_path, "w") as f:
                 f.write("%d %.3f" % (int(merged == full), t))
+        dist.barrier()
     finally:
+        if shm is not None:
+            shm.close()
         dist.destroy_process_group()
 
 
