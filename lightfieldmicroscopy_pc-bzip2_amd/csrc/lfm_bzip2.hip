@@ -120,6 +120,8 @@ struct Batch {
     uint32_t* rfreq;         // kMaxGroups * kMaxAlpha per stream
     uint32_t* words;         // out_cap / 4 per stream, MSB-first bit words
     uint32_t* out_bytes;
+    uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
+    uint32_t* wide_cnt;
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -1416,6 +1418,17 @@ __device__ __forceinline__ uint32_t run_digits(uint32_t z)
     return d;
 }
 
+// A (stream, table) heap is "narrow" when every node weight of
+// BZ2_hbMakeCodeLengths fits 17 bits: the table's frequencies sum to at most
+// nMTF, and each zero frequency counts 1.  Narrow heaps (nearly every default
+// 96x96x8 uint16 block: nMTF ~ 95-100k) take u32 entries in huff_lengths_heap,
+// the others u64 entries (rle2 lists those streams).
+constexpr uint32_t kNarrowWeight = 1u << 17;
+__device__ __forceinline__ bool heap_narrow(const Batch& B, uint32_t s, int alphaSize)
+{
+    return B.nmtf[s] + (uint32_t)alphaSize < kNarrowWeight;
+}
+
 constexpr int kRle2Threads = 256;
 constexpr uint32_t kRle2Per = 64;                        // m values per thread and tile
 constexpr uint32_t kRle2Tile = kRle2Threads * kRle2Per;  // 16384
@@ -1531,7 +1544,10 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         }
         __syncthreads();
     }
-    if (t == 0) B.nmtf[s] = s_wr;
+    if (t == 0) {
+        B.nmtf[s] = s_wr;
+        if (!heap_narrow(B, s, (int)nin + 2)) B.wide[atomicAdd(B.wide_cnt, 1u)] = s;  // u64 Huffman heaps
+    }
     for (uint32_t v = t; v < kMaxAlpha; v += kRle2Threads) B.mtf_freq[(size_t)s * kMaxAlpha + v] = freq[v];
 }
 
@@ -1725,6 +1741,9 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
 // weights as u32 (124 KiB for 48 lanes).  Leaf weights are recomputed from the
 // frequencies after a too-long retry (weight = 1 + weight / 2, per retry).
 constexpr int kLenTasks = 16;  // default lanes per wave (LFM_HUFF_LANES overrides: 1, 2, 4, 8, 16)
+
+
+// (LFM_HUFF_PACK=0; huff_lengths_heap below is the default)
 template <int kLenTasks>
 __global__ __launch_bounds__(64) void huff_lengths(Batch B)
 {
@@ -1732,9 +1751,10 @@ __global__ __launch_bounds__(64) void huff_lengths(Batch B)
     __shared__ uint16_t par[(2 * kMaxAlpha) * kLenTasks];
     __shared__ uint32_t heap_w[(kMaxAlpha + 2) * kLenTasks];
     const uint32_t lane = threadIdx.x;
-    const uint32_t task = blockIdx.x * kLenTasks + lane;
+    if (lane >= (uint32_t)kLenTasks) return;
+    auto run = [&](uint32_t task) {
     const uint32_t s = task / kMaxGroups, tb = task % kMaxGroups;
-    if (lane >= (uint32_t)kLenTasks || s >= B.nstreams || (B.flags[s] & kFlagHost) || tb >= B.ngroups[s]) return;
+    if (s >= B.nstreams || (B.flags[s] & kFlagHost) || tb >= B.ngroups[s]) return;
     const int alphaSize = (int)stream_nin(B, s) + 2;
     const uint32_t* freq = B.rfreq + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
     uint8_t* len = B.len + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
@@ -1817,9 +1837,201 @@ __global__ __launch_bounds__(64) void huff_lengths(Batch B)
         if (!tooLong) break;
         ++retries;
     }
+    };
+    run(blockIdx.x * kLenTasks + lane);
 #undef HN
 #undef HW
 #undef PA
+}
+
+// BZ2_hbMakeCodeLengths, kL (stream, table) heaps per wave, one per lane,
+// with wave-uniform heap walks.  A heap entry is one word: the weight as
+// (freq << 5 | height) above bit 10, the node in bits 0..9; the order of
+// (freq << 5 | height) is huffman.c's order of (freq << 8 | depth) because
+// height <= 17 -- a node of height 18 already means a code longer than
+// maxLen 17, so the lane keeps going on garbage and then redoes the tree with
+// halved weights, the retry huffman.c takes after building it.  Narrow heaps
+// (heap_narrow: weights < 2^17) use u32 entries (~1 KB of LDS per heap, so
+// many heaps are resident), the others u64 entries in a second launch over the
+// list the first one built (kList).
+//   * Entries sit in per-lane quads (entries 4q .. 4q + 3 contiguous): a
+//     node's children are half a quad, its grandchildren a whole quad, so a
+//     sift level reads the NEXT level's candidates (one ds_read_b128) while it
+//     decides the current one -- one LDS latency per level, not latency plus
+//     the compare chain.
+//   * The sift / upheap loops are uniform: every lane runs the level, selects
+//     instead of branches, one ballot per level (divergent per-lane exits cost
+//     ~20 scalar exec-mask instructions per level, and a CU's one scalar unit
+//     serves all its waves).
+//   * Parents go to global memory (the stream's code table, unused until
+//     huff_final) and come back for the depth pass, whose depths overlay the
+//     lane's own entries.
+template <typename Ent>
+struct HeapQuad {
+    Ent e[4];
+};
+
+constexpr int kHeapQuads = (kMaxAlpha + 2 + 3) / 4;  // entries 0 .. 259
+
+// kL heaps with Ent entries in the LDS area hb (kHeapQuads * kL quads);
+// this lane's heap is (stream s, table tb)
+template <typename Ent, int kL>
+__device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint32_t lane, uint32_t s, uint32_t tb)
+{
+    constexpr int kQuads = kHeapQuads;
+    constexpr uint32_t QB = sizeof(HeapQuad<Ent>);   // bytes per lane per quad
+    constexpr uint32_t QS = QB * kL;                 // bytes per quad row
+    constexpr uint32_t ES = sizeof(Ent);
+    const uint32_t lb = lane * QB;
+    auto ent = [&](uint32_t e) -> Ent& { return *(Ent*)(hb + (e >> 2) * QS + lb + (e & 3) * ES); };
+    {
+        const int A = (int)stream_nin(B, s) + 2;
+        const uint32_t* freq = B.rfreq + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
+        uint8_t* len = B.len + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
+        uint16_t* parent = (uint16_t*)(B.code + ((size_t)s * kMaxGroups + tb) * kMaxAlpha);  // nodes 1 .. 2A - 2
+        // depth of node k (<= 515): u16 number k % (ES / 2) of the lane's entry k / (ES / 2)
+        auto dep = [&](uint32_t k) -> uint16_t& {
+            return *(uint16_t*)((char*)&ent(k / (ES / 2)) + 2 * (k % (ES / 2)));
+        };
+        // rows are 8-byte aligned (258 words): pairs of words, a few loads ahead
+        auto ld2 = [](const void* p, int i) { return *(const uint2*)((const uint32_t*)p + (i > 0 ? i : 0)); };
+        // a < b on weights (bits 10 and up) <=> a < (b with its node bits cleared)
+        constexpr Ent kW = ~(Ent)1023;
+        // downheap from the root with key k; returns the new root.  Per level:
+        // the grandchildren quad is read first (it holds the children of
+        // either next node), then the level is decided from the children in
+        // registers; ea = address of the entry the key may land in, ca = the
+        // children pair of zz (ea of the next level is ca + 4 * right)
+        auto sift = [&](int nHeap, Ent k) {
+            uint32_t zz = 1, ea = lb + ES, ca = lb + 2u * ES;
+            Ent cx = ent(2), cy = ent(3), root = k;
+            bool go = true, first = true;
+            while (true) {
+                const uint32_t ga = min(zz, (uint32_t)kQuads - 1u) * QS + lb;
+                const HeapQuad<Ent> g = *(const HeapQuad<Ent>*)(hb + ga);
+                __builtin_amdgcn_sched_barrier(0);  // the read goes out before the level's compares
+                const uint32_t yy = zz << 1;
+                const bool r = yy < (uint32_t)nHeap && cy < (cx & kW);
+                const Ent ky = r ? cy : cx;
+                go = go && yy <= (uint32_t)nHeap && !(k < (ky & kW));
+                *(Ent*)(hb + ea) = ky;  // a stopped lane's stray write is overwritten below
+                if (first) root = go ? ky : k;
+                first = false;
+                ea = go ? ca + (r ? ES : 0u) : ea;
+                ca = ga + (r ? 2u * ES : 0u);
+                zz = go ? yy + (r ? 1u : 0u) : zz;
+                cx = r ? g.e[2] : g.e[0];
+                cy = r ? g.e[3] : g.e[1];
+                if (!__any(go)) break;
+            }
+            *(Ent*)(hb + ea) = k;
+            return root;
+        };
+        auto upheap = [&](uint32_t z, Ent k) {  // returns the final position
+            bool go = true;
+            while (true) {
+                const Ent up = ent(z >> 1);
+                go = go && k < (up & kW);  // the sentinel 0 stops it
+                ent(z) = go ? up : k;
+                z = go ? z >> 1 : z;
+                if (!__any(go)) break;
+            }
+            return z;
+        };
+        int retries = 0, nNodes = A;
+        while (true) {
+            // leaves at heap positions 1 .. A first (an insertion's upheap only
+            // touches positions below it), then inserted in order
+            ent(0) = 0;
+            // 32 frequencies per batch of 16 loads (one memory latency per
+            // batch, not per load: the compiler drains vmcnt at loop edges)
+            for (int i0 = 1; i0 <= A; i0 += 32) {
+                uint2 f[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) f[q] = ld2(freq, min(i0 - 1 + 2 * q, kMaxAlpha - 2));
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int i = i0 + 2 * q;
+                    uint32_t w0 = f[q].x ? f[q].x : 1u, w1 = f[q].y ? f[q].y : 1u;
+                    for (int r = 0; r < retries; ++r) {
+                        w0 = 1u + w0 / 2u;
+                        w1 = 1u + w1 / 2u;
+                    }
+                    if (i <= A) ent(i) = ((Ent)w0 << 15) | (Ent)i;
+                    if (i + 1 <= A) ent(i + 1) = ((Ent)w1 << 15) | (Ent)(i + 1);
+                }
+            }
+            for (int i = 1; i <= A; ++i) upheap((uint32_t)i, ent(i));
+            int nHeap = A;
+            nNodes = A;
+            uint32_t tooLong = 0;
+            Ent top = ent(1);
+            while (nHeap > 1) {
+                const Ent k1 = top;
+                const Ent k2 = sift(nHeap - 1, ent(nHeap));
+                --nHeap;
+                const Ent r2 = sift(nHeap - 1, ent(nHeap));
+                --nHeap;
+                ++nNodes;
+                parent[(uint32_t)k1 & 1023u] = (uint16_t)nNodes;
+                parent[(uint32_t)k2 & 1023u] = (uint16_t)nNodes;
+                const uint32_t h1 = (uint32_t)(k1 >> 10) & 31u, h2 = (uint32_t)(k2 >> 10) & 31u;
+                const uint32_t h = min(31u, 1u + max(h1, h2));
+                tooLong |= h > 17u ? 1u : 0u;
+                const Ent kn = ((((k1 >> 15) + (k2 >> 15)) << 5 | (Ent)h) << 10) | (Ent)nNodes;
+                ++nHeap;
+                top = upheap((uint32_t)nHeap, kn) == 1u ? kn : r2;
+            }
+            if (!tooLong) break;
+            ++retries;
+        }
+        if (retries) atomicAdd(B.wide_cnt + 1, (uint32_t)retries);  // statistics (LFM_BZ2_STATS)
+        // depths top-down (a parent is created after its children)
+        dep(nNodes) = 0;
+        // 64 parents per batch of 16 loads, highest nodes first
+        for (int kc = (nNodes - 1) & ~63; kc >= 0; kc -= 64) {
+            uint2 pw[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) pw[q] = ld2(parent, min(kc / 2 + 2 * q, (2 * kMaxAlpha) / 2 - 2));
+#pragma unroll
+            for (int q = 15; q >= 0; --q) {
+                const uint32_t p4[4] = {pw[q].x & 0xFFFFu, pw[q].x >> 16, pw[q].y & 0xFFFFu, pw[q].y >> 16};
+#pragma unroll
+                for (int r = 3; r >= 0; --r) {
+                    const int k = kc + 4 * q + r;
+                    if (k >= 1 && k < nNodes) dep(k) = (uint16_t)(dep(p4[r]) + 1u);
+                }
+            }
+        }
+        for (int i = 1; i <= A; ++i) len[i - 1] = (uint8_t)dep(i);
+    }
+}
+
+// Workgroups [0, nwg_wide): kL / 2 heaps of the wide streams (B.wide,
+// listed by rle2 and counted by the host) with u64 entries, first so their
+// chains start first; the rest: kL (stream, table) heaps each with u32
+// entries (lanes of wide streams exit).  One launch, so a wide heap's chain
+// runs beside the narrow ones.
+template <int kL>
+__global__ __launch_bounds__(64) void huff_lengths_heap(Batch B, uint32_t nwg_wide, uint32_t nwide_streams)
+{
+    __shared__ HeapQuad<uint32_t> hq[kHeapQuads * kL];
+    char* hb = (char*)hq;
+    const uint32_t lane = threadIdx.x;
+    if (blockIdx.x >= nwg_wide) {
+        const uint32_t task = (blockIdx.x - nwg_wide) * kL + lane;
+        const uint32_t s = task / kMaxGroups, tb = task % kMaxGroups;
+        if (lane >= (uint32_t)kL || s >= B.nstreams || (B.flags[s] & kFlagHost) || tb >= B.ngroups[s]) return;
+        if (!heap_narrow(B, s, (int)stream_nin(B, s) + 2)) return;
+        heap_code_lengths<uint32_t, kL>(B, hb, lane, s, tb);
+    } else {
+        constexpr int kW = kL / 2;
+        const uint32_t i = blockIdx.x * kW + lane;
+        if (lane >= (uint32_t)kW || i >= nwide_streams * kMaxGroups) return;
+        const uint32_t s = B.wide[i / kMaxGroups], tb = i % kMaxGroups;
+        if ((B.flags[s] & kFlagHost) || tb >= B.ngroups[s]) return;
+        heap_code_lengths<uint64_t, kW>(B, hb, lane, s, tb);
+    }
 }
 
 // One wave per stream.  Selector MTF (compress.c, 6 entries): the list is a
@@ -2363,8 +2575,9 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * out_cap, 256);             // words
     b += align_up((size_t)nstreams * kMaxAlpha * 4, 256);       // mtf_freq
     b += align_up((size_t)nstreams * 8 * 4, 256);               // inuse
+    b += align_up((size_t)nstreams * kMaxGroups * 4 + 64, 256);  // wide heap list
     b += 16 * align_up((size_t)nstreams * 4 + 64, 256);         // small per-stream arrays
-    b += align_up(((size_t)nstreams + 1) * 8 + 16, 256);        // offsets + counters
+    b += align_up(((size_t)nstreams + 1) * 8 + 32, 256);        // offsets + counters
     b += align_up(prim_tmp_bytes(nstreams, cap), 256);          // rocPRIM temporary storage
     return b;
 }
@@ -2434,11 +2647,12 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.words = (uint32_t*)take((size_t)count * B.out_cap);
     B.mtf_freq = (uint32_t*)take((size_t)count * kMaxAlpha * 4);
     B.inuse = (uint32_t*)take((size_t)count * 8 * 4);
+    B.wide = (uint32_t*)take((size_t)count * kMaxGroups * 4 + 64);
     uint32_t** small[] = {&B.raw_len, &B.n, &B.crc, &B.flags, &B.done, &B.seg_begin, &B.seg_end, &B.nmtf,
                           &B.orig_ptr, &B.nsel, &B.ngroups, &B.out_bytes};
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
     for (int k = (int)(sizeof(small) / sizeof(small[0])); k < 16; ++k) (void)take((size_t)count * 4 + 64);
-    uint64_t* offs = (uint64_t*)take(((size_t)count + 1) * 8 + 16);
+    uint64_t* offs = (uint64_t*)take(((size_t)count + 1) * 8 + 32);
     size_t tmp_bytes = prim_tmp_bytes(count, B.cap);
     void* tmp = take(tmp_bytes);
 
@@ -2456,7 +2670,10 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         hipLaunchKernelGGL(rle1_crc<false>, dim3(count), dim3(kRleThreads), 0, st, B);
     }
     if (!ok()) return LFM_HIP_ERUNTIME;
-    uint32_t* d_cnt = (uint32_t*)(offs + count + 1);  // two counters after offs
+    // counters after offs: [0..2] chunk classes of the bucket pass, then the
+    // tied-list counts [0], [1]; [3] wide Huffman streams, [4] Huffman retries
+    uint32_t* d_cnt = (uint32_t*)(offs + count + 1);
+    B.wide_cnt = d_cnt + 3;
     // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
     {
         ChunkLists CL;
@@ -2467,7 +2684,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         CL.cnt = d_cnt;
         uint32_t nch[3] = {0, 0, 0};
-        if (hipMemsetAsync(d_cnt, 0, 12, st) != hipSuccess ||
+        if (hipMemsetAsync(d_cnt, 0, 32, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         static const uint32_t bkt_bits = [] {
@@ -2635,6 +2852,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             hipLaunchKernelGGL(mtf_win, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
         hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
     }
+    // streams whose Huffman weights need u64 heap entries (listed by rle2)
+    uint32_t nwide = 0;
+    if (!ok() || hipMemcpyAsync(&nwide, B.wide_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess || nwide > count)
+        return LFM_HIP_ERUNTIME;
     static const bool hsel = !(std::getenv("LFM_HSEL") && std::atoi(std::getenv("LFM_HSEL")) == 0);
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
     for (int it = 0; it < kIters; ++it) {
@@ -2645,13 +2867,32 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             const int x = v ? std::atoi(v) : kLenTasks;
             return (x == 1 || x == 2 || x == 4 || x == 8 || x == 16) ? x : kLenTasks;
         }();
+        // uniform heaps, u32 entries for the narrow tables and u64 for the
+        // streams rle2 listed, in one launch (LFM_HUFF_PACK = heaps per
+        // workgroup, 32 by default; 0 = the per-lane branchy kernel below)
+        static const int plane = [] {
+            const char* v = std::getenv("LFM_HUFF_PACK");
+            const int x = v ? std::atoi(v) : 32;
+            return (x == 0 || x == 4 || x == 8 || x == 16 || x == 32) ? x : 32;
+        }();
         const dim3 g((count * kMaxGroups + lanes - 1) / lanes);
-        switch (lanes) {
-        case 1: hipLaunchKernelGGL(huff_lengths<1>, g, dim3(64), 0, st, B); break;
-        case 2: hipLaunchKernelGGL(huff_lengths<2>, g, dim3(64), 0, st, B); break;
-        case 4: hipLaunchKernelGGL(huff_lengths<4>, g, dim3(64), 0, st, B); break;
-        case 8: hipLaunchKernelGGL(huff_lengths<8>, g, dim3(64), 0, st, B); break;
-        default: hipLaunchKernelGGL(huff_lengths<16>, g, dim3(64), 0, st, B); break;
+        if (plane) {
+            const uint32_t nn = (count * kMaxGroups + plane - 1) / plane;
+            const uint32_t nw = (nwide * kMaxGroups + plane / 2 - 1) / (plane / 2);
+            switch (plane) {
+            case 4: hipLaunchKernelGGL(huff_lengths_heap<4>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
+            case 8: hipLaunchKernelGGL(huff_lengths_heap<8>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
+            case 32: hipLaunchKernelGGL(huff_lengths_heap<32>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
+            default: hipLaunchKernelGGL(huff_lengths_heap<16>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
+            }
+        } else {
+            switch (lanes) {
+            case 1: hipLaunchKernelGGL(huff_lengths<1>, g, dim3(64), 0, st, B); break;
+            case 2: hipLaunchKernelGGL(huff_lengths<2>, g, dim3(64), 0, st, B); break;
+            case 4: hipLaunchKernelGGL(huff_lengths<4>, g, dim3(64), 0, st, B); break;
+            case 8: hipLaunchKernelGGL(huff_lengths<8>, g, dim3(64), 0, st, B); break;
+            default: hipLaunchKernelGGL(huff_lengths<16>, g, dim3(64), 0, st, B); break;
+            }
         }
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
@@ -2659,6 +2900,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(1024), 0, st, B.out_bytes, count, offs);
     hipLaunchKernelGGL(compact_streams, dim3(count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
     if (!ok()) return LFM_HIP_ERUNTIME;
+    static const bool stats = std::getenv("LFM_BZ2_STATS") && std::atoi(std::getenv("LFM_BZ2_STATS")) != 0;
+    if (stats) {
+        uint32_t c[8] = {};
+        if (hipMemcpyAsync(c, d_cnt, 32, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
+            std::fprintf(stderr, "lfm_bzip2 stats: %u streams, %u with u64 Huffman heaps, Huffman retries %u\n", count,
+                         c[3], c[4]);
+    }
     std::vector<uint32_t> nbytes(count);
     if (hipMemcpyAsync(nbytes.data(), B.out_bytes, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemcpyAsync(h_flags, B.flags, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||

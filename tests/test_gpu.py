@@ -326,6 +326,13 @@ def _bz2_cases():
     cases["run_lengths"] = np.concatenate(runs)
     allb = np.concatenate([np.full(1 + (i % 7), i, np.uint8) for i in range(256)] * 20 + [np.array([5], np.uint8)])
     cases["all_bytes"] = allb  # every byte value in use (not periodic: one extra byte)
+    # nMTF >= 2^17: the Huffman tables' weights leave the packed heap's 17 bits
+    cases["random_wide"] = rng.integers(0, 256, 160000, dtype=np.uint8)
+    # geometric byte distribution: code lengths beyond 17 in the first tree
+    # (the weight-halving retry of BZ2_hbMakeCodeLengths)
+    geo = np.minimum(rng.geometric(0.5, 140000) - 1, 40).astype(np.uint8)
+    cases["geometric"] = geo
+    cases["geometric_small"] = geo[:30000].copy()
     return cases
 
 
@@ -339,8 +346,8 @@ def test_gpu_bzip2_matches_libbz2_edge_cases(lfmlib, oracle, gpu):
         for level in (1, 2, 9):
             got, flags = lfmlib.bzip2_device(d, [n, 1, 1, 1, 1], [n, 1, 1, 1, 1], 1, level=level)
             exp = ref_bz2(oracle, data.tobytes(), level)
-            if flags[0]:
-                assert name.startswith("periodic"), (name, level)
+            if flags[0]:  # periodic, or a second bzip2 block (nblockMAX = 100000 * level - 19)
+                assert name.startswith("periodic") or n >= 100000 * level - 19, (name, level)
                 continue
             assert not name.startswith("periodic"), name
             assert got[0] == exp, (name, level, len(got[0]), len(exp))
@@ -360,6 +367,22 @@ def test_gpu_bzip2_block_grid_and_symbols(lfmlib, oracle, gpu):
     for (i, coord, size), g in zip(blocks, got):
         raw = oracle.gather_block(sym[None, None], coord, size)
         assert g == ref_bz2(oracle, raw, 1), i
+
+
+def test_gpu_bzip2_many_wide_heaps(lfmlib, oracle, gpu):
+    """200 random 160 kB streams: 1 200 Huffman tables whose weights leave the
+    packed heap's 17 bits, more than one pass of the wide-heap kernel's grid;
+    mixed with low-entropy streams (packed heaps) in the same batch."""
+    torch = gpu
+    rng = np.random.default_rng(11)
+    n, ns = 160000, 200
+    img = rng.integers(0, 256, (ns, n), dtype=np.uint8)
+    img[::7] = rng.integers(0, 4, (len(img[::7]), n), dtype=np.uint8)
+    d = torch.from_numpy(img.reshape(-1).copy()).cuda()
+    got, flags = lfmlib.bzip2_device(d, [n, 1, ns, 1, 1], [n, 1, 1, 1, 1], 1)
+    assert not any(flags)
+    for i in range(ns):
+        assert got[i] == ref_bz2(oracle, img[i].tobytes(), 2), i
 
 
 def test_gpu_bzip2_host_fallback_streams(lfmlib, oracle, gpu):
