@@ -66,6 +66,22 @@ LFM_API int lfm_encoder_encode(lfm_encoder* enc, const void* img, int img_is_dev
                                const char metadata[KLB_METADATA_SIZE], const uint8_t** out, uint64_t* out_len,
                                lfm_encode_stats* stats);
 
+/* Pipelined encode of a stack (z0 = 0, prev_frame = NULL) or of a z-slab
+ * (arguments as lfm_encoder_encode_slab).  Returns once every kernel of the
+ * encode has run (img may be released), with the .lfm's last payload copies
+ * still running on a system DMA engine; the caller can submit the next stack
+ * at once and its GPU work overlaps those copies.  At most two encodes are in
+ * flight: a submit first waits for the copies of the one before last.
+ * *ticket names the encode for lfm_encoder_wait. */
+LFM_API int lfm_encoder_submit(lfm_encoder* enc, const void* img, int img_is_device, const void* prev_frame,
+                               uint32_t z0, const uint32_t xyzct[KLB_DATA_DIMS], int dataType, int headerVersion,
+                               int Nnum, const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                               const char metadata[KLB_METADATA_SIZE], uint64_t* ticket);
+/* Wait for a submitted encode.  *out stays valid until the second submit
+ * after it (or a synchronous encode on this encoder); returns its status. */
+LFM_API int lfm_encoder_wait(lfm_encoder* enc, uint64_t ticket, const uint8_t** out, uint64_t* out_len,
+                             lfm_encode_stats* stats);
+
 /* Encode z-slab [z0, z0 + xyzct[2]) of a larger stack (c = t = 1) for
  * multi-GPU sharding: frame z of the slab is temporal when video & (z0 + z)
  * is odd, and the slab's first frame then uses prev_frame (the raw frame

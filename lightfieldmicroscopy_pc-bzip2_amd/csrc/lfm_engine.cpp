@@ -435,6 +435,7 @@ Encoder::Encoder(int device) : device_(device) {}
 
 Encoder::~Encoder()
 {
+    join_inflight();
     if (gpu_ready_) {
         (void)hipSetDevice(device_);
         if (d_in_) (void)hipFree(d_in_);
@@ -443,7 +444,8 @@ Encoder::~Encoder()
         if (d_prev_) (void)hipFree(d_prev_);
         for (BzSlot& sl : bz_) {
             if (sl.d_ws) (void)hipFree(sl.d_ws);
-            if (sl.d_out) (void)hipFree(sl.d_out);
+            for (void* d : sl.d_out)
+                if (d) (void)hipFree(d);
             if (sl.h_out) (void)hipHostFree(sl.h_out);
             if (sl.stream) (void)hipStreamDestroy(sl.stream);
         }
@@ -451,7 +453,81 @@ Encoder::~Encoder()
         if (ev0_) (void)hipEventDestroy(ev0_);
         if (ev1_) (void)hipEventDestroy(ev1_);
         if (stream_) (void)hipStreamDestroy(stream_);
+        if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     }
+}
+
+void Encoder::join_inflight()
+{
+    for (Inflight& f : fly_)
+        if (f.th.joinable()) f.th.join();
+}
+
+int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads, const SlabSpec* slab,
+                    uint64_t* ticket)
+{
+    static const bool trace = std::getenv("LFM_TRACE_SUBMIT") && std::atoi(std::getenv("LFM_TRACE_SUBMIT")) != 0;
+    auto ts = [](const char* what) {
+        std::fprintf(stderr, "[submit %.3f] %s\n",
+                     std::chrono::duration<double, std::milli>(clk::now().time_since_epoch()).count(), what);
+    };
+    if (trace) ts("enter");
+    const int p = par_;
+    Inflight& f = fly_[p];
+    if (f.th.joinable()) f.th.join();  // the encode before last used these buffers
+    if (trace) ts("joined before-last");
+    f.ticket = next_ticket_++;
+    f.rc = 0;
+    f.d2h_ms = 0;
+    std::memset(&f.st, 0, sizeof(f.st));
+    if (ticket) *ticket = f.ticket;
+    std::vector<CopyJob> jobs;
+    MemSink sink(&mem_ring[p]);
+    defer_ = &jobs;
+    f.rc = encode(img, dev, h, sink, &f.st, threads, slab);
+    defer_ = nullptr;
+    par_ ^= 1;
+    if (trace) ts("encoded");
+    if (f.rc || jobs.empty()) return f.rc;
+    // PCIe is one link: the previous encode's copies go first
+    Inflight& g = fly_[p ^ 1];
+    if (g.th.joinable()) g.th.join();
+    if (trace) ts("joined previous");
+    f.th = std::thread([this, &f, jobs]() {
+        (void)hipSetDevice(device_);
+        auto t0 = clk::now();
+        for (const CopyJob& j : jobs) {
+            if (sdma_d2h(j.dst, j.src, j.n)) continue;
+            if (!copy_stream_ && hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking) != hipSuccess) {
+                f.rc = 3;
+                break;
+            }
+            if (hipMemcpyAsync(j.dst, j.src, j.n, hipMemcpyDeviceToHost, copy_stream_) != hipSuccess ||
+                hipStreamSynchronize(copy_stream_) != hipSuccess) {
+                f.rc = 3;
+                break;
+            }
+        }
+        f.d2h_ms = ms_since(t0);
+    });
+    if (trace) ts("finisher started");
+    return 0;
+}
+
+int Encoder::wait(uint64_t ticket, const PinnedBuffer** out, lfm_encode_stats* st)
+{
+    for (int p = 0; p < 2; ++p) {
+        Inflight& f = fly_[p];
+        if (f.ticket != ticket || ticket == 0) continue;
+        if (f.th.joinable()) f.th.join();
+        if (out) *out = &mem_ring[p];
+        if (st) {
+            *st = f.st;
+            st->d2h_ms += f.d2h_ms;
+        }
+        return f.rc;
+    }
+    return 3;  // not submitted, or two submits ago
 }
 
 int Encoder::ensure_gpu()
@@ -703,7 +779,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         BzSlot& sl = bz_[k];
         if (!sl.stream && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) return 3;
         if (!dev_alloc(sl.d_ws, sl.d_ws_cap, ws)) return 3;
-        if (!dev_alloc(sl.d_out, sl.d_out_cap, batch * out_cap)) return 3;
+        if (!dev_alloc(sl.d_out[par_], sl.d_out_cap[par_], batch * out_cap)) return 3;
         if (!sl.h_out || sl.h_out_cap < batch * out_cap) {
             if (sl.h_out) (void)hipHostFree(sl.h_out);
             sl.h_out = nullptr;
@@ -744,7 +820,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             sizes[b].assign(cnt, 0);
             flags[b].assign(cnt, 0);
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
-                                          ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
+                                          ws, sl.d_out[par_], sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
             bool any_flag = false;
             for (uint32_t i = 0; i < cnt; ++i) any_flag |= flags[b][i] != 0;
             staged[b] = !direct || any_flag;
@@ -752,7 +828,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                 uint64_t tot = 0;
                 for (uint32_t i = 0; i < cnt; ++i) tot += sizes[b][i];
                 auto t0 = clk::now();
-                ok = payload_d2h(sl.h_out, sl.d_out, tot, sl.stream);
+                ok = payload_d2h(sl.h_out, sl.d_out[par_], tot, sl.stream);
                 d2h[k] += ms_since(t0);
             }
             {
@@ -785,9 +861,15 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             for (uint32_t i = 0; i < cnt; ++i) tot += sizes[b][i];
             BzSlot& sl = bz_[b % nslots];
             uint8_t* dst = sink.direct(tot);
-            auto t0 = clk::now();
-            if (!dst || !payload_d2h(dst, sl.d_out, tot, sl.stream)) rc = 3;
-            if (st) st->d2h_ms += ms_since(t0);
+            if (!dst) {
+                rc = 3;
+            } else if (defer_ && b + nslots >= nbatch) {  // last round: the finisher copies (submit)
+                defer_->push_back({dst, sl.d_out[par_], tot});
+            } else {
+                auto t0 = clk::now();
+                if (!payload_d2h(dst, sl.d_out[par_], tot, sl.stream)) rc = 3;
+                if (st) st->d2h_ms += ms_since(t0);
+            }
             for (uint32_t i = 0; i < cnt; ++i) {
                 offset += sizes[b][i];
                 h.blockOffset[b0 + i] = offset;
@@ -875,6 +957,7 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
                     const SlabSpec* slab)
 {
     static const SlabSpec whole;
+    if (!defer_) join_inflight();  // a synchronous encode may reuse every output buffer
     if (threads <= 0) threads = default_threads();
     auto t0 = clk::now();
     if (st) std::memset(st, 0, sizeof(*st));

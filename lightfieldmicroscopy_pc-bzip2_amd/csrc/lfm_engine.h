@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <hip/hip_runtime.h>
 #include "klb_imageHeader.h"
@@ -125,6 +126,17 @@ public:
                const SlabSpec* slab = nullptr);
     PinnedBuffer mem_out;
     int device() const { return device_; }
+    // Pipelined encodes (lfm_encoder_submit / lfm_encoder_wait): the payload
+    // copies of an encode's last round of bzip2 batches run on a finisher
+    // thread while the caller starts the next encode, which builds into the
+    // other device / pinned output buffers -- at most two encodes in flight.
+    // The input may be released when submit returns (every kernel is done).
+    int submit(const void* img, bool dev, klb_image_header& h, int threads, const SlabSpec* slab, uint64_t* ticket);
+    // wait for a submitted encode: its .lfm is *out (valid until the second
+    // submit after it); stats as encode() reports them, d2h_ms including the
+    // deferred copies
+    int wait(uint64_t ticket, const PinnedBuffer** out, lfm_encode_stats* st);
+    PinnedBuffer mem_ring[2];
     // predictor selection on one host frame (uploaded to this encoder's device)
     int select_host_frame(const void* frame, int W, int H, int T, int family, int* chosen, float entropy[8]);
 
@@ -134,6 +146,24 @@ private:
     int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level);
     int ensure_gpu();
     void* dev_alloc(void*& p, size_t& cap, size_t need);
+    void join_inflight();
+    struct CopyJob {
+        void* dst;
+        const void* src;
+        size_t n;
+    };
+    struct Inflight {
+        uint64_t ticket = 0;  // 0: none
+        std::thread th;       // the deferred payload copies
+        int rc = 0;
+        double d2h_ms = 0;
+        lfm_encode_stats st{};
+    };
+    Inflight fly_[2];                         // by output parity
+    uint64_t next_ticket_ = 1;
+    int par_ = 0;                             // output parity (d_out of the slots) of the encode being built
+    std::vector<CopyJob>* defer_ = nullptr;   // set while submit() builds an encode
+    hipStream_t copy_stream_ = nullptr;       // copies the SDMA path cannot take
     int device_;
     bool gpu_ready_ = false;
     hipStream_t stream_ = nullptr;
@@ -147,7 +177,7 @@ private:
     struct BzSlot {
         hipStream_t stream = nullptr;
         void* d_ws = nullptr; size_t d_ws_cap = 0;
-        void* d_out = nullptr; size_t d_out_cap = 0;
+        void* d_out[2] = {nullptr, nullptr}; size_t d_out_cap[2] = {0, 0};  // by output parity
         void* h_out = nullptr; size_t h_out_cap = 0;
     };
     BzSlot bz_[kBzSlots];

@@ -36,7 +36,8 @@ EXPORTS = [
     "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
     "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_set_devices", "lfm_get_devices",
-    "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab",
+    "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab", "lfm_encoder_submit",
+    "lfm_encoder_wait",
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
@@ -99,6 +100,10 @@ def lib():
                                           ctypes.c_int, ctypes.c_int, u32p, ctypes.c_int, ctypes.c_char_p,
                                           ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
+    L.lfm_encoder_submit.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_uint32, u32p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, u32p, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+    L.lfm_encoder_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
+                                   ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
     L.lfm_encoder_encode_multi.argtypes = [vp, vp, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p,
                                            ctypes.c_int, ctypes.c_char_p,
                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
@@ -328,6 +333,38 @@ class Encoder:
                                       _meta(metadata), ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
         _check(rc, "lfm_encoder_encode")
         del keep
+        if not copy:
+            return memoryview((ctypes.c_uint8 * n.value).from_address(ctypes.addressof(out.contents))), st.as_dict()
+        return ctypes.string_at(out, n.value), st.as_dict()
+
+    def submit(self, img, z0=0, prev=None, header_version=0, nnum=13, block_size=None, compression=1,
+               metadata=None, xyzct=None, data_type=None):
+        """Pipelined encode (lfm_encoder_submit) of a stack (z0 = 0) or a z-slab:
+        returns a ticket once every kernel has run (img may be released); the
+        .lfm's last payload copies finish in the background.  wait(ticket)
+        gives (.lfm, stats); at most two encodes are in flight."""
+        ptr, dev, xyzct, data_type, keep = self._operand(img, xyzct, data_type)
+        pptr = None
+        if prev is not None:
+            pptr, pdev, _, _, pkeep = self._operand(prev, [1, 1, 1, 1, 1], data_type)
+            if pdev != dev:
+                raise LfmError("prev must live where img lives (host or device)")
+        t = ctypes.c_uint64()
+        rc = lib().lfm_encoder_submit(self._h, ptr, dev, pptr, int(z0), _u32(xyzct), data_type, int(header_version),
+                                      int(nnum), _u32(block_size) if block_size is not None else None, compression,
+                                      _meta(metadata), ctypes.byref(t))
+        _check(rc, "lfm_encoder_submit")
+        del keep
+        return t.value
+
+    def wait(self, ticket, copy=True):
+        """(.lfm, stats) of a submitted encode; with copy=False a zero-copy
+        memoryview valid until the second submit after it."""
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_uint64()
+        st = EncodeStats()
+        rc = lib().lfm_encoder_wait(self._h, ticket, ctypes.byref(out), ctypes.byref(n), ctypes.byref(st))
+        _check(rc, "lfm_encoder_wait")
         if not copy:
             return memoryview((ctypes.c_uint8 * n.value).from_address(ctypes.addressof(out.contents))), st.as_dict()
         return ctypes.string_at(out, n.value), st.as_dict()

@@ -536,3 +536,41 @@ def test_roi_read_small_blocks_gpu(lfmlib, oracle, gpu, tmp_path):
                 assert np.array_equal(out, img[lb[2]:ub[2] + 1, lb[1]:ub[1] + 1, lb[0]:ub[0] + 1]), (fam, video, lb, ub)
         finally:
             lfmlib.set_family("tiles")
+
+
+def test_pipelined_submit_wait(lfmlib, oracle, gpu):
+    """lfm_encoder_submit / lfm_encoder_wait: two encodes in flight (the
+    second builds while the first's payload copies run) give the same bytes as
+    synchronous encodes of the same stacks -- stacks and slabs, device and host
+    input; a ticket two submits old is refused; a synchronous encode after
+    submits still works."""
+    torch = gpu
+    stacks = [oracle.synthetic_lf(480, 400, Z=24, T=15, seed=100 + i)[0, 0] for i in range(4)]
+    lfmlib.set_family("angle")
+    try:
+        sync = lfmlib.Encoder(device=0)
+        exp = [sync.encode(s, header_version=0, nnum=15)[0] for s in stacks]
+        exp_slab = sync.encode_slab(stacks[0][8:], 8, header_version=8 + 4, nnum=15)[0]
+        sync.close()
+        enc = lfmlib.Encoder(device=0)
+        tickets = []
+        got = {}
+        for i, s in enumerate(stacks):
+            img = dev16(torch, s) if i % 2 == 0 else s
+            tickets.append(enc.submit(img, header_version=0, nnum=15))
+            del img
+            if i >= 1:
+                got[i - 1] = enc.wait(tickets[i - 1])[0]
+        got[3] = enc.wait(tickets[3])[0]
+        assert [got[i] for i in range(4)] == exp
+        assert enc.wait(tickets[3])[0] == exp[3]  # waiting twice is fine
+        with pytest.raises(lfmlib.LfmError):
+            enc.wait(tickets[1])  # two submits ago: its buffers are reused
+        t = enc.submit(dev16(torch, stacks[0][8:]), z0=8, header_version=8 + 4, nnum=15)
+        b, st = enc.wait(t)
+        assert b == exp_slab and st["out_bytes"] == len(b)
+        b2, _ = enc.encode(stacks[1], header_version=0, nnum=15)
+        assert b2 == exp[1]
+        enc.close()
+    finally:
+        lfmlib.set_family("tiles")
