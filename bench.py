@@ -353,6 +353,13 @@ def main():
     }
     if place_ms:
         line["stages_ms"]["place_ms"] = round(float(np.mean(place_ms[-args.steps:])), 3)
+    # GPU bzip2 stages (HIP events per HIP stream, max over the two streams that
+    # run concurrently) and their rate in block bytes
+    bz_in = stats[-1]["bz_in_bytes"]
+    for name in ("rle1", "bwt", "mtf", "huffman", "emit"):
+        ms = float(np.mean([s["bz_stage_ms"][name] for s in stats]))
+        line["stages_ms"]["bz_%s_ms" % name] = round(ms, 3)
+        line["stages_ms"]["bz_%s_GBps" % name] = round(bz_in / (ms / 1e3) / 1e9, 1) if ms > 0 else None
     # byte check of the last timed .lfm against the oracle (outside the timed region)
     if rank == 0:
         buf = b if shm is None else shm.buf[:shm.len]

@@ -49,6 +49,9 @@ typedef struct lfm_encode_stats {
     int header_version;   /* final header byte                                */
     float entropy[8];     /* candidate entropies when auto-selected, else 0   */
     uint64_t out_bytes;   /* size of the .lfm produced                        */
+    double bz_stage_ms[5];/* GPU bzip2 stages (lfm_hip_bzip2_last_stage_ms order), HIP events,
+                             summed over a HIP stream's batches, max over the streams */
+    uint64_t bz_in_bytes; /* block bytes the GPU bzip2 stage compressed       */
 } lfm_encode_stats;
 
 typedef struct lfm_encoder lfm_encoder;

@@ -80,6 +80,11 @@ size_t lfm_hip_bzip2_workspace_bytes(uint32_t count, uint32_t block_bytes);
 int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], const uint32_t bs[5], uint32_t bpp,
                          uint32_t first, uint32_t count, uint32_t level, void* d_ws, size_t ws_bytes,
                          void* d_payload, uint64_t* h_sizes, uint32_t* h_flags, void* stream);
+/* Stage times (HIP events on its stream, ms) of the calling thread's last
+ * lfm_hip_bzip2_blocks: [0] RLE1 + CRC, [1] BWT (buckets, chunk sorts, tie
+ * rounds), [2] MTF + RUNA/RUNB, [3] Huffman tables, [4] bit emission +
+ * compaction.  Returns 0, or 3 when no call has completed on this thread. */
+int lfm_hip_bzip2_last_stage_ms(float ms[5]);
 
 /* GPU bzip2 decode of `count` single-block streams (the .lfm block payloads,
  * SURVEY.md 8(f2); replaces the per-block BZ2_bzBuffToBuffDecompress of

@@ -2525,6 +2525,31 @@ void ensure_crc_table()
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// stage boundary events of the calling thread (lfm_hip_bzip2_last_stage_ms)
+struct StageEvents {
+    int dev = -1;
+    hipEvent_t ev[6] = {};
+    float last_ms[5] = {};
+    bool valid = false;
+    ~StageEvents()
+    {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    bool ready(int d)
+    {
+        if (dev == d) return true;
+        for (hipEvent_t& e : ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) return false;
+        }
+        dev = d;
+        return true;
+    }
+};
+thread_local StageEvents t_stage;
+
 // rocPRIM temporary storage for the largest use of each primitive in a batch
 // of `count` streams (size queries only: no device work).  Carved out of the
 // caller's workspace: a per-call stream-ordered allocation of these
@@ -2604,6 +2629,12 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             return LFM_HIP_ERUNTIME;
         crc_dev = dev;
     }
+    StageEvents& SE = t_stage;
+    SE.valid = false;
+    const bool timed = SE.ready(dev);
+    auto mark = [&](int i) {
+        if (timed) (void)hipEventRecord(SE.ev[i], st);
+    };
     Batch B{};
     B.img = (const uint8_t*)d_img;
     uint32_t raw_cap = bpp;
@@ -2663,6 +2694,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     // blocks); other geometries gather the blocks first
     const bool from_img = ((uintptr_t)d_img & 15) == 0 && (bs[0] * bpp) % 16 == 0 && (dims[0] * bpp) % 16 == 0 &&
                           ((dims[0] % bs[0]) * bpp) % 16 == 0;
+    mark(0);
     if (from_img) {
         hipLaunchKernelGGL(rle1_crc<true>, dim3(count), dim3(kRleThreads), 0, st, B);
     } else {
@@ -2671,9 +2703,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     }
     if (!ok()) return LFM_HIP_ERUNTIME;
     // counters after offs: [0..2] chunk classes of the bucket pass, then the
-    // tied-list counts [0], [1]; [3] wide Huffman streams, [4] Huffman retries
+    // tied-list counts [0], [1]; [3] wide Huffman streams, [4] Huffman
+    // retries
     uint32_t* d_cnt = (uint32_t*)(offs + count + 1);
     B.wide_cnt = d_cnt + 3;
+    mark(1);
     // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
     {
         ChunkLists CL;
@@ -2736,13 +2770,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         if (!ok()) return LFM_HIP_ERUNTIME;
     }
+    uint32_t* cl = B.cl0;
+    uint32_t* cl_next = B.cl1;
     if (e == hipSuccess) {
         hipLaunchKernelGGL(tie_offsets, dim3(1), dim3(1024), 0, st, B, d_cnt);
         hipLaunchKernelGGL(tie_compact, dim3(count), dim3(256), 0, st, B, B.cl0);
         if (!ok()) return LFM_HIP_ERUNTIME;
     }
-    uint32_t* cl = B.cl0;
-    uint32_t* cl_next = B.cl1;
     uint32_t covered = kKeyBytes;
     uint32_t* d_cnt2 = d_cnt + 1;
     // text rounds over the tied list (group keys: u64 per entry in the rank
@@ -2839,6 +2873,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         h *= 2;
     }
     if (e != hipSuccess) return LFM_HIP_ERUNTIME;
+    mark(2);
     {
         const uint32_t nseg_max = (B.cap + kSeg - 1) / kSeg;
         int32_t* seg_last = (int32_t*)B.keys_a;  // free after the BWT (count * nseg_max KiB << N * 8 bytes)
@@ -2857,6 +2892,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (!ok() || hipMemcpyAsync(&nwide, B.wide_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess || nwide > count)
         return LFM_HIP_ERUNTIME;
+    mark(3);
     static const bool hsel = !(std::getenv("LFM_HSEL") && std::atoi(std::getenv("LFM_HSEL")) == 0);
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
     for (int it = 0; it < kIters; ++it) {
@@ -2896,9 +2932,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
+    mark(4);
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(1024), 0, st, B.out_bytes, count, offs);
     hipLaunchKernelGGL(compact_streams, dim3(count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
+    mark(5);
     if (!ok()) return LFM_HIP_ERUNTIME;
     static const bool stats = std::getenv("LFM_BZ2_STATS") && std::atoi(std::getenv("LFM_BZ2_STATS")) != 0;
     if (stats) {
@@ -2913,5 +2951,17 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         hipStreamSynchronize(st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
     for (uint32_t i = 0; i < count; ++i) h_sizes[i] = nbytes[i];
+    if (timed) {
+        SE.valid = true;
+        for (int i = 0; i < 5; ++i)
+            if (hipEventElapsedTime(&SE.last_ms[i], SE.ev[i], SE.ev[i + 1]) != hipSuccess) SE.valid = false;
+    }
     return LFM_HIP_OK;
+}
+
+extern "C" int lfm_hip_bzip2_last_stage_ms(float ms[5])
+{
+    if (!ms || !t_stage.valid) return 3;
+    for (int i = 0; i < 5; ++i) ms[i] = t_stage.last_ms[i];
+    return 0;
 }

@@ -14,6 +14,7 @@
 #include "lfm_engine.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -806,6 +807,8 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     std::condition_variable cv;
     std::atomic<bool> abort_all{false};
     std::vector<double> d2h(nslots, 0.0);
+    std::vector<std::array<double, 5>> stage_ms(nslots);  // per slot, summed over its batches
+    for (auto& a : stage_ms) a.fill(0.0);
     auto worker = [&](int k) {
         (void)hipSetDevice(device_);
         BzSlot& sl = bz_[k];
@@ -821,6 +824,9 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             flags[b].assign(cnt, 0);
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
                                           ws, sl.d_out[par_], sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
+            float sm[5];
+            if (ok && lfm_hip_bzip2_last_stage_ms(sm) == 0)
+                for (int i = 0; i < 5; ++i) stage_ms[k][i] += sm[i];
             bool any_flag = false;
             for (uint32_t i = 0; i < cnt; ++i) any_flag |= flags[b][i] != 0;
             staged[b] = !direct || any_flag;
@@ -920,8 +926,12 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     }
     cv.notify_all();
     for (auto& t : pool) t.join();
-    if (st)
+    if (st) {
         for (double v : d2h) st->d2h_ms += v;
+        for (int i = 0; i < 5; ++i)
+            for (int k = 0; k < nslots; ++k) st->bz_stage_ms[i] = std::max(st->bz_stage_ms[i], stage_ms[k][i]);
+        st->bz_in_bytes = nblocks * (uint64_t)block_bytes;
+    }
     if (rc) return rc;
     return sink.finish(h);
 }

@@ -41,7 +41,7 @@ EXPORTS = [
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
-    "lfm_hip_bzip2_blocks", "lfm_hip_bunzip2_workspace_bytes", "lfm_hip_bunzip2_blocks", "lfm_hip_scatter_blocks",
+    "lfm_hip_bzip2_blocks", "lfm_hip_bzip2_last_stage_ms", "lfm_hip_bunzip2_workspace_bytes", "lfm_hip_bunzip2_blocks", "lfm_hip_scatter_blocks",
 ]
 
 
@@ -53,11 +53,13 @@ class EncodeStats(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
                 ("predict_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double), ("compress_ms", ctypes.c_double),
                 ("chosen", ctypes.c_int), ("header_version", ctypes.c_int), ("entropy", ctypes.c_float * 8),
-                ("out_bytes", ctypes.c_uint64)]
+                ("out_bytes", ctypes.c_uint64), ("bz_stage_ms", ctypes.c_double * 5), ("bz_in_bytes", ctypes.c_uint64)]
+    BZ_STAGES = ("rle1", "bwt", "mtf", "huffman", "emit")
 
     def as_dict(self):
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "entropy"}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("entropy", "bz_stage_ms")}
         d["entropy"] = list(self.entropy)
+        d["bz_stage_ms"] = dict(zip(self.BZ_STAGES, list(self.bz_stage_ms)))
         return d
 
 
