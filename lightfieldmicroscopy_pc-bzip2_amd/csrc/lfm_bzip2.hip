@@ -1404,19 +1404,9 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
     }
 }
 
-// zero-run digits of a run of z zeros (compress.c: z-1, then RUNA/RUNB by
-// bit, (z-2)/2 ... : bijective base 2)
-__device__ __forceinline__ uint32_t run_digits(uint32_t z)
-{
-    uint32_t d = 0;
-    uint32_t zp = z - 1;
-    while (true) {
-        ++d;
-        if (zp < 2) break;
-        zp = (zp - 2) / 2;
-    }
-    return d;
-}
+// zero-run digits of a run of z >= 1 zeros (compress.c: z-1, then RUNA/RUNB
+// by bit, (z-2)/2 ... : bijective base 2, whose length is floor(log2(z + 1)))
+__device__ __forceinline__ uint32_t run_digits(uint32_t z) { return 31u - (uint32_t)__clz(z + 1u); }
 
 // A (stream, table) heap is "narrow" when every node weight of
 // BZ2_hbMakeCodeLengths fits 17 bits: the table's frequencies sum to at most
