@@ -85,6 +85,11 @@ int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], const uint32
  * rounds), [2] MTF + RUNA/RUNB, [3] Huffman tables, [4] bit emission +
  * compaction.  Returns 0, or 3 when no call has completed on this thread. */
 int lfm_hip_bzip2_last_stage_ms(float ms[5]);
+/* Progress hook of the calling thread's lfm_hip_bzip2_blocks calls: fn(ctx,
+ * stage) once the device has finished stage 1 (BWT) and stage 2 (MTF + RUNA/
+ * RUNB), i.e. at the host synchronisations that follow them; fn == NULL
+ * removes it.  The pipelined encoder starts the next stack's kernels there. */
+void lfm_hip_bzip2_set_stage_hook(void (*fn)(void* ctx, int stage), void* ctx);
 
 /* GPU bzip2 decode of `count` single-block streams (the .lfm block payloads,
  * SURVEY.md 8(f2); replaces the per-block BZ2_bzBuffToBuffDecompress of

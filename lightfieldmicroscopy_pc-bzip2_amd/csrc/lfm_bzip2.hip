@@ -2539,6 +2539,8 @@ struct StageEvents {
     }
 };
 thread_local StageEvents t_stage;
+thread_local void (*t_hook)(void*, int) = nullptr;
+thread_local void* t_hook_ctx = nullptr;
 
 // rocPRIM temporary storage for the largest use of each primitive in a batch
 // of `count` streams (size queries only: no device work).  Carved out of the
@@ -2864,6 +2866,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     }
     if (e != hipSuccess) return LFM_HIP_ERUNTIME;
     mark(2);
+    if (t_hook) t_hook(t_hook_ctx, 1);  // the doubling / tie rounds above end with a host synchronisation
     {
         const uint32_t nseg_max = (B.cap + kSeg - 1) / kSeg;
         int32_t* seg_last = (int32_t*)B.keys_a;  // free after the BWT (count * nseg_max KiB << N * 8 bytes)
@@ -2883,6 +2886,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         hipStreamSynchronize(st) != hipSuccess || nwide > count)
         return LFM_HIP_ERUNTIME;
     mark(3);
+    if (t_hook) t_hook(t_hook_ctx, 2);  // after the wide-stream count's synchronisation: rle2 has run
     static const bool hsel = !(std::getenv("LFM_HSEL") && std::atoi(std::getenv("LFM_HSEL")) == 0);
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
     for (int it = 0; it < kIters; ++it) {
@@ -2947,6 +2951,12 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             if (hipEventElapsedTime(&SE.last_ms[i], SE.ev[i], SE.ev[i + 1]) != hipSuccess) SE.valid = false;
     }
     return LFM_HIP_OK;
+}
+
+extern "C" void lfm_hip_bzip2_set_stage_hook(void (*fn)(void*, int), void* ctx)
+{
+    t_hook = fn;
+    t_hook_ctx = ctx;
 }
 
 extern "C" int lfm_hip_bzip2_last_stage_ms(float ms[5])

@@ -440,17 +440,19 @@ Encoder::~Encoder()
     if (gpu_ready_) {
         (void)hipSetDevice(device_);
         if (d_in_) (void)hipFree(d_in_);
-        if (d_sym_) (void)hipFree(d_sym_);
+        for (void* d : d_sym_)
+            if (d) (void)hipFree(d);
         if (d_ws_) (void)hipFree(d_ws_);
         if (d_prev_) (void)hipFree(d_prev_);
-        for (BzSlot& sl : bz_) {
-            if (sl.d_ws) (void)hipFree(sl.d_ws);
-            for (void* d : sl.d_out)
-                if (d) (void)hipFree(d);
-            if (sl.h_out) (void)hipHostFree(sl.h_out);
-            if (sl.stream) (void)hipStreamDestroy(sl.stream);
-        }
-        if (h_sym_) (void)hipHostFree(h_sym_);
+        for (auto& set : bz_)
+            for (BzSlot& sl : set) {
+                if (sl.d_ws) (void)hipFree(sl.d_ws);
+                if (sl.d_out) (void)hipFree(sl.d_out);
+                if (sl.h_out) (void)hipHostFree(sl.h_out);
+                if (sl.stream) (void)hipStreamDestroy(sl.stream);
+            }
+        for (void* hs : h_sym_)
+            if (hs) (void)hipHostFree(hs);
         if (ev0_) (void)hipEventDestroy(ev0_);
         if (ev1_) (void)hipEventDestroy(ev1_);
         if (stream_) (void)hipStreamDestroy(stream_);
@@ -464,6 +466,42 @@ void Encoder::join_inflight()
         if (f.th.joinable()) f.th.join();
 }
 
+void Encoder::Inflight::release()
+{
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        released = true;
+    }
+    cv.notify_all();
+}
+
+void Encoder::Inflight::reach()
+{
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        ++reached;
+        if (need > 0 && reached >= need) released = true;
+    }
+    cv.notify_all();
+}
+
+void Encoder::Inflight::wait_release()
+{
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return released; });
+}
+
+// release stage of the pipelined encodes (lfm_hip_bzip2_set_stage_hook stages)
+static int pipe_release_stage()
+{
+    static const int v = [] {
+        const char* e = std::getenv("LFM_PIPE_AT");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 0 && x <= 2 ? x : 0;
+    }();
+    return v;
+}
+
 int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads, const SlabSpec* slab,
                     uint64_t* ticket)
 {
@@ -473,45 +511,60 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
                      std::chrono::duration<double, std::milli>(clk::now().time_since_epoch()).count(), what);
     };
     if (trace) ts("enter");
+    static const SlabSpec whole;
+    if (threads <= 0) threads = default_threads();
     const int p = par_;
     Inflight& f = fly_[p];
-    if (f.th.joinable()) f.th.join();  // the encode before last used these buffers
-    if (trace) ts("joined before-last");
+    if (f.th.joinable()) f.th.join();  // the encode before last used this buffer set
+    fly_[p ^ 1].wait_release();        // the previous encode is in its tail
+    if (trace) ts("released");
     f.ticket = next_ticket_++;
     f.rc = 0;
-    f.d2h_ms = 0;
     std::memset(&f.st, 0, sizeof(f.st));
+    {
+        std::lock_guard<std::mutex> lk(f.mu);
+        f.reached = 0;
+        f.need = 0;
+        f.released = false;
+    }
     if (ticket) *ticket = f.ticket;
-    std::vector<CopyJob> jobs;
-    MemSink sink(&mem_ring[p]);
-    defer_ = &jobs;
-    f.rc = encode(img, dev, h, sink, &f.st, threads, slab);
-    defer_ = nullptr;
     par_ ^= 1;
-    if (trace) ts("encoded");
-    if (f.rc || jobs.empty()) return f.rc;
-    // PCIe is one link: the previous encode's copies go first
-    Inflight& g = fly_[p ^ 1];
-    if (g.th.joinable()) g.th.join();
-    if (trace) ts("joined previous");
-    f.th = std::thread([this, &f, jobs]() {
+    auto t0 = clk::now();
+    int level = slab ? slab->level : -1;
+    if (level < 1 && slab && slab->z0 > 0 && h.getBytesPerPixel()) {
+        klb_image_header nominal(h);
+        for (int d = 0; d < KLB_DATA_DIMS; ++d)
+            if (d != 2 && nominal.blockSize[d]) nominal.blockSize[d] = std::min(nominal.blockSize[d], h.xyzct[d]);
+        if (nominal.blockSize[2] == 0) nominal.blockSize[2] = 1;
+        level = bzip2_level(nominal);
+    }
+    const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
+    if (!gpu_bz) {  // no GPU bzip2: the whole encode here
+        MemSink sink(&mem_ring[p]);
+        f.rc = encode_set(img, dev, h, sink, &f.st, threads, slab, p);
+        f.release();
+        return f.rc;
+    }
+    const uint8_t* dsym = nullptr;
+    if ((f.rc = normalize_header(h)) || (f.rc = predictor_stage(img, dev, h, nullptr, &dsym, &f.st, slab ? *slab : whole, p)) ||
+        (f.rc = ensure_gpu())) {
+        f.release();
+        return f.rc;
+    }
+    if (trace) ts("predicted");
+    auto hh = std::make_shared<klb_image_header>(h);
+    f.th = std::thread([this, &f, hh, dsym, level, p, t0]() {
         (void)hipSetDevice(device_);
-        auto t0 = clk::now();
-        for (const CopyJob& j : jobs) {
-            if (sdma_d2h(j.dst, j.src, j.n)) continue;
-            if (!copy_stream_ && hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking) != hipSuccess) {
-                f.rc = 3;
-                break;
-            }
-            if (hipMemcpyAsync(j.dst, j.src, j.n, hipMemcpyDeviceToHost, copy_stream_) != hipSuccess ||
-                hipStreamSynchronize(copy_stream_) != hipSuccess) {
-                f.rc = 3;
-                break;
-            }
-        }
-        f.d2h_ms = ms_since(t0);
+        MemSink sink(&mem_ring[p]);
+        auto tc = clk::now();
+        f.rc = gpu_compress(dsym, *hh, sink, &f.st, level, p, &f);
+        f.st.compress_ms = ms_since(tc);
+        f.st.total_ms = ms_since(t0);
+        f.st.header_version = hh->headerVersion;
+        f.st.chosen = hh->headerVersion & 0x7F;
+        f.st.out_bytes = hh->getCompressedFileSizeInBytes();
+        f.release();  // in case the release stage was never reached (host paths)
     });
-    if (trace) ts("finisher started");
     return 0;
 }
 
@@ -522,10 +575,7 @@ int Encoder::wait(uint64_t ticket, const PinnedBuffer** out, lfm_encode_stats* s
         if (f.ticket != ticket || ticket == 0) continue;
         if (f.th.joinable()) f.th.join();
         if (out) *out = &mem_ring[p];
-        if (st) {
-            *st = f.st;
-            st->d2h_ms += f.d2h_ms;
-        }
+        if (st) *st = f.st;
         return f.rc;
     }
     return 3;  // not submitted, or two submits ago
@@ -562,8 +612,12 @@ void* Encoder::dev_alloc(void*& p, size_t& cap, size_t need)
 }
 
 int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym,
-                             const uint8_t** dsym, lfm_encode_stats* st, const SlabSpec& slab)
+                             const uint8_t** dsym, lfm_encode_stats* st, const SlabSpec& slab, int set)
 {
+    void*& d_sym_ = this->d_sym_[set];
+    size_t& d_sym_cap_ = this->d_sym_cap_[set];
+    void*& h_sym_ = this->h_sym_[set];
+    size_t& h_sym_cap_ = this->h_sym_cap_[set];
     // dsym != nullptr: the caller compresses on the GPU -- leave the symbols
     // of every volume in device memory (*dsym) and skip the host copy.
     const bool keep = dsym != nullptr;
@@ -736,8 +790,12 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
 // GPU bzip2 of every block (lfm_bzip2.hip), streams batched to bound the
 // workspace; streams the device hands back (RLE1 block reaching nblockMAX,
 // periodic blocks) are compressed by libbz2 here.  Same bytes either way.
-int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level)
+int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level,
+                          int set, Inflight* fly)
 {
+    void*& h_sym_ = this->h_sym_[set];
+    size_t& h_sym_cap_ = this->h_sym_cap_[set];
+    BzSlot* bz_ = this->bz_[set];
     const BlockGrid g(h);
     const uint64_t nblocks = g.nblocks;
     h.resizeBlockOffset(nblocks);
@@ -780,7 +838,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         BzSlot& sl = bz_[k];
         if (!sl.stream && hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking) != hipSuccess) return 3;
         if (!dev_alloc(sl.d_ws, sl.d_ws_cap, ws)) return 3;
-        if (!dev_alloc(sl.d_out[par_], sl.d_out_cap[par_], batch * out_cap)) return 3;
+        if (!dev_alloc(sl.d_out, sl.d_out_cap, batch * out_cap)) return 3;
         if (!sl.h_out || sl.h_out_cap < batch * out_cap) {
             if (sl.h_out) (void)hipHostFree(sl.h_out);
             sl.h_out = nullptr;
@@ -809,10 +867,29 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     std::vector<double> d2h(nslots, 0.0);
     std::vector<std::array<double, 5>> stage_ms(nslots);  // per slot, summed over its batches
     for (auto& a : stage_ms) a.fill(0.0);
+    // pipelined encodes: the next submit starts once every batch of the last
+    // round has passed the release stage (hook of lfm_hip_bzip2_blocks)
+    const int release_at = pipe_release_stage();
+    struct HookCtx {
+        Inflight* fly;
+        int stage;
+    };
+    HookCtx hctx{fly, release_at};
+    if (fly) {
+        std::lock_guard<std::mutex> lk(fly->mu);
+        fly->need = (int)std::min<uint64_t>(nslots, nbatch);
+    }
     auto worker = [&](int k) {
         (void)hipSetDevice(device_);
         BzSlot& sl = bz_[k];
         for (uint64_t b = k; b < nbatch; b += nslots) {
+            if (fly && release_at > 0 && b + nslots >= nbatch)
+                lfm_hip_bzip2_set_stage_hook(
+                    [](void* ctx, int stage) {
+                        HookCtx* c = (HookCtx*)ctx;
+                        if (stage == c->stage) c->fly->reach();
+                    },
+                    &hctx);
             if (b >= (uint64_t)nslots) {  // wait until the writer consumed batch b - nslots
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return state[b - nslots] != 1 || abort_all.load(); });
@@ -823,7 +900,11 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             sizes[b].assign(cnt, 0);
             flags[b].assign(cnt, 0);
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
-                                          ws, sl.d_out[par_], sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
+                                          ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
+            if (fly && b + nslots >= nbatch) {
+                if (release_at == 0) fly->reach();
+                lfm_hip_bzip2_set_stage_hook(nullptr, nullptr);
+            }
             float sm[5];
             if (ok && lfm_hip_bzip2_last_stage_ms(sm) == 0)
                 for (int i = 0; i < 5; ++i) stage_ms[k][i] += sm[i];
@@ -834,7 +915,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                 uint64_t tot = 0;
                 for (uint32_t i = 0; i < cnt; ++i) tot += sizes[b][i];
                 auto t0 = clk::now();
-                ok = payload_d2h(sl.h_out, sl.d_out[par_], tot, sl.stream);
+                ok = payload_d2h(sl.h_out, sl.d_out, tot, sl.stream);
                 d2h[k] += ms_since(t0);
             }
             {
@@ -869,11 +950,9 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             uint8_t* dst = sink.direct(tot);
             if (!dst) {
                 rc = 3;
-            } else if (defer_ && b + nslots >= nbatch) {  // last round: the finisher copies (submit)
-                defer_->push_back({dst, sl.d_out[par_], tot});
             } else {
                 auto t0 = clk::now();
-                if (!payload_d2h(dst, sl.d_out[par_], tot, sl.stream)) rc = 3;
+                if (!payload_d2h(dst, sl.d_out, tot, sl.stream)) rc = 3;
                 if (st) st->d2h_ms += ms_since(t0);
             }
             for (uint32_t i = 0; i < cnt; ++i) {
@@ -966,8 +1045,14 @@ int Encoder::select_host_frame(const void* frame, int W, int H, int T, int famil
 int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
                     const SlabSpec* slab)
 {
+    join_inflight();  // a synchronous encode may use either buffer set
+    return encode_set(img, dev, h, sink, st, threads, slab, 0);
+}
+
+int Encoder::encode_set(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st,
+                        int threads, const SlabSpec* slab, int set)
+{
     static const SlabSpec whole;
-    if (!defer_) join_inflight();  // a synchronous encode may reuse every output buffer
     if (threads <= 0) threads = default_threads();
     auto t0 = clk::now();
     if (st) std::memset(st, 0, sizeof(*st));
@@ -986,12 +1071,12 @@ int Encoder::encode(const void* img, bool dev, klb_image_header& h, Sink& sink, 
     const uint8_t* sym = nullptr;
     const uint8_t* dsym = nullptr;
     const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
-    int rc = predictor_stage(img, dev, h, &sym, gpu_bz ? &dsym : nullptr, st, slab ? *slab : whole);
+    int rc = predictor_stage(img, dev, h, &sym, gpu_bz ? &dsym : nullptr, st, slab ? *slab : whole, set);
     if (rc) return rc;
     auto tc = clk::now();
     if (gpu_bz) {
         if ((rc = ensure_gpu())) return rc;
-        rc = gpu_compress(dsym, h, sink, st, level);
+        rc = gpu_compress(dsym, h, sink, st, level, set, nullptr);
     } else {
         rc = compress_blocks(sym, h, sink, threads, level);
     }

@@ -1,6 +1,8 @@
 // lfm_engine.h -- encode / decode engine behind klb_imageIO, the C ABI and
 // the lfm_encoder API.
 #pragma once
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
@@ -126,11 +128,18 @@ public:
                const SlabSpec* slab = nullptr);
     PinnedBuffer mem_out;
     int device() const { return device_; }
-    // Pipelined encodes (lfm_encoder_submit / lfm_encoder_wait): the payload
-    // copies of an encode's last round of bzip2 batches run on a finisher
-    // thread while the caller starts the next encode, which builds into the
-    // other device / pinned output buffers -- at most two encodes in flight.
-    // The input may be released when submit returns (every kernel is done).
+    // Pipelined encodes (lfm_encoder_submit / lfm_encoder_wait), two buffer
+    // sets (symbols, bzip2 slots and workspaces, pinned output) used in turn:
+    // submit runs the predictor stage of its stack into one set and hands the
+    // GPU bzip2 + in-order assembly + payload copies to a finisher thread.
+    // The next submit starts once the previous encode's batches have passed
+    // the release stage (env LFM_PIPE_AT: 0 = when its kernels are done, the
+    // default, so the next stack's kernels overlap its assembly and payload
+    // copies; 1 = after its BWT, 2 = after its MTF, so they also overlap its
+    // latency-bound tail -- measured 8 943 / 9 035 vs 9 098 Mpixel/s: the
+    // heap chains slow down as much as the head gains).  At most two encodes
+    // are in flight.  The input may be released when submit returns (the
+    // predictor stage has consumed it).
     int submit(const void* img, bool dev, klb_image_header& h, int threads, const SlabSpec* slab, uint64_t* ticket);
     // wait for a submitted encode: its .lfm is *out (valid until the second
     // submit after it); stats as encode() reports them, d2h_ms including the
@@ -141,47 +150,53 @@ public:
     int select_host_frame(const void* frame, int W, int H, int T, int family, int* chosen, float entropy[8]);
 
 private:
+    // an encode in flight (submit): its finisher thread and the release point
+    struct Inflight {
+        uint64_t ticket = 0;  // 0: none
+        std::thread th;       // GPU bzip2, in-order assembly, payload copies
+        int rc = 0;
+        lfm_encode_stats st{};
+        std::mutex mu;
+        std::condition_variable cv;
+        int reached = 0;      // batches of the last round past the release stage
+        int need = 0;         // ... needed to release the next submit (0: not yet known)
+        bool released = true;
+        void release();
+        void wait_release();
+        void reach();         // one last-round batch passed the release stage
+    };
     int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, const uint8_t** dsym,
-                        lfm_encode_stats* st, const SlabSpec& slab);
-    int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level);
+                        lfm_encode_stats* st, const SlabSpec& slab, int set);
+    int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level, int set,
+                     Inflight* fly);
+    int encode_set(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
+                   const SlabSpec* slab, int set);
     int ensure_gpu();
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     void join_inflight();
-    struct CopyJob {
-        void* dst;
-        const void* src;
-        size_t n;
-    };
-    struct Inflight {
-        uint64_t ticket = 0;  // 0: none
-        std::thread th;       // the deferred payload copies
-        int rc = 0;
-        double d2h_ms = 0;
-        lfm_encode_stats st{};
-    };
-    Inflight fly_[2];                         // by output parity
+    Inflight fly_[2];                         // by buffer set
     uint64_t next_ticket_ = 1;
-    int par_ = 0;                             // output parity (d_out of the slots) of the encode being built
-    std::vector<CopyJob>* defer_ = nullptr;   // set while submit() builds an encode
-    hipStream_t copy_stream_ = nullptr;       // copies the SDMA path cannot take
+    int par_ = 0;                             // buffer set of the next submit
+    hipStream_t copy_stream_ = nullptr;       // payload copies the SDMA path cannot take
     int device_;
     bool gpu_ready_ = false;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
     void* d_in_ = nullptr;  size_t d_in_cap_ = 0;
-    void* d_sym_ = nullptr; size_t d_sym_cap_ = 0;
+    void* d_sym_[2] = {nullptr, nullptr}; size_t d_sym_cap_[2] = {0, 0};  // by buffer set
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
     void* d_prev_ = nullptr; size_t d_prev_cap_ = 0;
-    // GPU bzip2 pipeline slots (stream, workspace, device + pinned output)
-    static constexpr int kBzSlots = 4;  // HIP streams available to the bzip2 pipeline (LFM_BZ2_SLOTS picks how many run)
+    // GPU bzip2 pipeline slots (stream, workspace, device + pinned output),
+    // kBzSlots per buffer set (LFM_BZ2_SLOTS picks how many run, at most that)
+    static constexpr int kBzSlots = 4;
     struct BzSlot {
         hipStream_t stream = nullptr;
         void* d_ws = nullptr; size_t d_ws_cap = 0;
-        void* d_out[2] = {nullptr, nullptr}; size_t d_out_cap[2] = {0, 0};  // by output parity
+        void* d_out = nullptr; size_t d_out_cap = 0;
         void* h_out = nullptr; size_t h_out_cap = 0;
     };
-    BzSlot bz_[kBzSlots];
-    void* h_sym_ = nullptr; size_t h_sym_cap_ = 0;   // pinned
+    BzSlot bz_[2][kBzSlots];
+    void* h_sym_[2] = {nullptr, nullptr}; size_t h_sym_cap_[2] = {0, 0};   // pinned, by buffer set
 };
 
 // process-wide encoders for the C ABI / klb_imageIO, one per (device, worker
