@@ -70,12 +70,14 @@ LFM_API int lfm_encoder_encode(lfm_encoder* enc, const void* img, int img_is_dev
                                lfm_encode_stats* stats);
 
 /* Pipelined encode of a stack (z0 = 0, prev_frame = NULL) or of a z-slab
- * (arguments as lfm_encoder_encode_slab).  Returns once every kernel of the
- * encode has run (img may be released), with the .lfm's last payload copies
- * still running on a system DMA engine; the caller can submit the next stack
- * at once and its GPU work overlaps those copies.  At most two encodes are in
- * flight: a submit first waits for the copies of the one before last.
- * *ticket names the encode for lfm_encoder_wait. */
+ * (arguments as lfm_encoder_encode_slab).  Runs the predictor stage (img may
+ * be released on return), then hands the GPU bzip2 stage, the .lfm assembly
+ * and its payload copies (system DMA engine) to a finisher thread and
+ * returns.  The next submit's GPU work starts once this encode's kernels are
+ * done (env LFM_PIPE_AT: 1 / 2 start it after the BWT / MTF instead).  At
+ * most two encodes are in flight: a submit first joins the one before last.
+ * *ticket names the encode for lfm_encoder_wait; errors of the finisher are
+ * returned by lfm_encoder_wait. */
 LFM_API int lfm_encoder_submit(lfm_encoder* enc, const void* img, int img_is_device, const void* prev_frame,
                                uint32_t z0, const uint32_t xyzct[KLB_DATA_DIMS], int dataType, int headerVersion,
                                int Nnum, const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
