@@ -312,7 +312,7 @@ def main():
     alg_bytes = px_rank * 4  # 2 B read + 2 B written per pixel (no temporal frames in this config)
     achieved = alg_bytes / (pred_ms / 1e3) / 1e9
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "r01_traffic_predict.json")
+    tpath = os.path.join(REPO, "profiles", "r02_traffic_predict.json")
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
