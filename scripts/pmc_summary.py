@@ -50,6 +50,12 @@ def main():
         out[k] = d
     res = {"source": args.pmc_dir, "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 wide-read half count); "
                                                   "WRITE_SIZE KiB x1024", "kernels": out}
+    if len(out) == 1:  # one kernel: its per-launch HBM figures at the top (bench.py reads them)
+        (k, d), = out.items()
+        res["kernel"] = k
+        for f in ("hbm_read_bytes_per_launch", "hbm_write_bytes_per_launch", "hbm_bytes_per_launch"):
+            if f in d:
+                res[f] = d[f]
     if args.algorithmic_read is not None:
         res["algorithmic_read_bytes"] = args.algorithmic_read
     if args.algorithmic_write is not None:
