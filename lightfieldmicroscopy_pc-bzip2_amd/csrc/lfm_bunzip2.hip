@@ -18,9 +18,11 @@
 //               stable), tt[LF(i)] = i << 8 | ll[LF(i)] (decompress.c's fast
 //               tt), and the inverse BWT as a parallel walk: markers every kMark
 //               nodes of the cycle (plus its start, tt[origPtr] >> 8), each
-//               walker follows tt from its marker to the next one and counts,
-//               one lane chains the segments to their output offsets, the
-//               walkers walk again and write the RLE1 text.
+//               walker follows tt from its marker to the next one, counting and
+//               keeping the first kWalkKeep bytes it passes, one lane chains the
+//               segments to their output offsets, the kept bytes are copied into
+//               place (a wave per segment) and only the rare longer segments
+//               are walked again from where their walker stopped keeping.
 //   bzd_rle1    one wave per stream: RLE1 decode (4 equal bytes + a count) into
 //               the output block from 64 text segments (their start states
 //               resolved by running every start state), CRC-32 of the block in
@@ -43,6 +45,8 @@ constexpr int kMaxSel = 18002;
 constexpr int kMaxLen = 20;
 constexpr int kLutBits = 10;
 constexpr uint32_t kMark = 128;  // cycle nodes per inverse-BWT walker (on average)
+constexpr uint32_t kWalkKeep = 512;  // bytes a walker keeps from its one walk (segments are
+                                     // geometric, mean kMark: 1.8 % of them are longer)
 
 // flags
 constexpr uint32_t kHost = 1;      // decode with the host library
@@ -64,6 +68,8 @@ struct Dec {
     uint32_t* mnext;
     uint32_t* mlen;
     uint32_t* mstart;
+    uint32_t* mres;           // node a walker stopped keeping bytes at (segments > kWalkKeep)
+    uint8_t* wkeep;           // kWalkKeep bytes per walker
     uint32_t* n;
     uint32_t* orig;
     uint32_t* crc;
@@ -538,16 +544,31 @@ __global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
     const bool extra = (v0 % kMark) != 0;
     const uint32_t nwalk = nm + (extra ? 1u : 0u);
     auto node_of = [&](uint32_t id) { return id < nm ? id * kMark : v0; };
-    // pass 1: segment lengths and successors
+    uint32_t* mres = D.mres + (size_t)s * D.mcap;
+    uint8_t* keep = D.wkeep + (size_t)s * D.mcap * kWalkKeep;
+    // pass 1: segment lengths and successors; the walker keeps the bytes it
+    // passes (the low byte of each tt entry it reads) in dwords
     for (uint32_t id = t; id < nwalk; id += kTtThreads) {
-        uint32_t pos = node_of(id), len = 0, nx = ~0u;
+        uint32_t pos = node_of(id), len = 0, nx = ~0u, acc = 0, res = 0;
+        uint32_t* kp = (uint32_t*)(keep + (size_t)id * kWalkKeep);
         do {
-            pos = tt[pos] >> 8;
+            if (len == kWalkKeep) res = pos;
+            const uint32_t e = tt[pos];
+            if (len < kWalkKeep) {
+                acc |= (e & 0xFFu) << (8 * (len & 3u));
+                if ((len & 3u) == 3u) {
+                    kp[len >> 2] = acc;
+                    acc = 0;
+                }
+            }
+            pos = e >> 8;
             ++len;
             nx = marker_id(pos, v0, nm);
         } while (nx == ~0u && len <= n);
+        if (len < kWalkKeep && (len & 3u)) kp[len >> 2] = acc;
         mnext[id] = nx;
         mlen[id] = len;
+        mres[id] = res;
     }
     __syncthreads();
     // chain the segments from the start (one lane)
@@ -566,13 +587,21 @@ __global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
         if (t == 0) D.flags[s] = kHost;  // not one cycle: not a valid bzip2 block
         return;
     }
-    // pass 2: the RLE1 text, segment by segment
+    // pass 2: the kept bytes into place, one wave per segment
+    const uint32_t lane = t & 63, wave = t >> 6;
+    for (uint32_t id = wave; id < nwalk; id += kTtThreads / 64) {
+        const uint32_t o = mstart[id], m = min(mlen[id], kWalkKeep);
+        const uint8_t* src = keep + (size_t)id * kWalkKeep;
+        for (uint32_t k = lane; k < m; k += 64) rle[o + k] = src[k];
+    }
+    // segments longer than kWalkKeep: walk on from where their walker stopped keeping
     for (uint32_t id = t; id < nwalk; id += kTtThreads) {
-        uint32_t pos = node_of(id), o = mstart[id];
         const uint32_t len = mlen[id];
-        for (uint32_t k = 0; k < len; ++k) {
+        if (len <= kWalkKeep) continue;
+        uint32_t pos = mres[id], o = mstart[id] + kWalkKeep;
+        for (uint32_t k = kWalkKeep; k < len; ++k) {
             const uint32_t e = tt[pos];
-            rle[o + k] = (uint8_t)e;
+            rle[o++] = (uint8_t)e;
             pos = e >> 8;
         }
     }
@@ -812,7 +841,8 @@ extern "C" size_t lfm_hip_bunzip2_workspace_bytes(uint32_t count, uint32_t out_s
     b += al(((size_t)count + 1) * 8);
     b += al((size_t)count * cap);          // ll, then the RLE1 text (ll is dead once tt holds its bytes)
     b += al((size_t)count * cap * 4);      // tt
-    b += 3 * al((size_t)count * mc * 4);
+    b += 4 * al((size_t)count * mc * 4);
+    b += al((size_t)count * mc * kWalkKeep);  // walkers' kept bytes
     b += 6 * al((size_t)count * 4 + 64);
     return b;
 }
@@ -872,6 +902,8 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     D.mnext = (uint32_t*)take((size_t)count * D.mcap * 4);
     D.mlen = (uint32_t*)take((size_t)count * D.mcap * 4);
     D.mstart = (uint32_t*)take((size_t)count * D.mcap * 4);
+    D.mres = (uint32_t*)take((size_t)count * D.mcap * 4);
+    D.wkeep = take((size_t)count * D.mcap * kWalkKeep);
     uint32_t** small[] = {&D.n, &D.orig, &D.crc, &D.flags, &D.out_len};
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
     (void)take((size_t)count * 4 + 64);
