@@ -135,11 +135,17 @@ struct BitReader {
 //    (~300 symbols) before they are needed; a refill is one readlane (a
 //    scalar-register queue made the compiler wait for every refill load right
 //    where it was issued);
-//  * output bytes collect in a register (one byte per lane) and leave in
-//    64-byte stores; a RUNA/RUNB run fills lanes of it, long runs are written
-//    by all 64 lanes;
-//  * one flat loop per symbol (one bit-window advance, run digits accumulate
-//    until the next non-run symbol), so the per-symbol code stays short.
+//  * the symbols go a group (50 symbols, one Huffman table) at a time: the
+//    Huffman loop only decodes (symbol k of the group into lane k), then the
+//    lanes work out the RUNA/RUNB digits (digit j of a run adds (sym + 1) << j
+//    copies of the list front, so each digit lane owns its own stretch of the
+//    output), the move-to-front chain runs over the group's non-run symbols
+//    only (s_ff1 over their ballot), a prefix sum over the lanes gives every
+//    lane its output offset and the lanes store their bytes.  The per-symbol
+//    scalar code is a third of the earlier single loop's (which did the run
+//    bookkeeping, the move to front and a 64-byte output staging per symbol),
+//    and the decode is bound by that code: ~16 waves per CU share one scalar
+//    unit (PMC: 43 SALU + 20 VALU + 11 branch instructions per symbol before).
 // Output: the BWT last column ll[], n, origPtr, the block CRC.
 struct WaveBits {
     const uint32_t* w;   // the stream's first (aligned) payload word
@@ -326,109 +332,102 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             __syncthreads();
         }
         if (flag) break;
-        // symbols
-        uint32_t mtfw = s2u;   // the move-to-front list, as output bytes
-        uint32_t obuf = 0;     // pending output bytes, byte i of the batch in lane i
-        uint32_t op = 0;       // pending bytes (they belong at ll[nblock - op ..])
+        // symbols, a group at a time
+        uint32_t mtfw = s2u;   // the move-to-front list, as output bytes, 4 per lane
         const uint32_t EOB = nInUse + 1;
         const uint32_t cap = D.cap;
-        uint32_t g = 0, gleft = 0, tb = 0, selw = 0;
-        uint32_t es = 0, rs = 0;  // pending RUNA/RUNB run: length, next digit
+        const uint64_t ltmask = (1ull << lane) - 1ull;
         const int kk0 = 1 - 4 * (int)lane;
-        // one exit, at the bottom: an error sets flag and the iteration runs on
-        // harmlessly (no write past cap), so the loop stays a simple loop (with
-        // an exit per error the compiler threaded a state code through every
-        // iteration)
-        uint32_t sym = 0;
-        do {
-            if (gleft == 0) {  // next group of 50 symbols: its table
-                flag |= (g >= nSel || br.over()) ? kHost : 0u;
-                if ((g & 7) == 0) selw = U(sel[g >> 3]);
-                tb = ((selw >> (4 * (g & 7))) & 15u) << LB;
-                ++g;
-                gleft = 50;
-            }
-            --gleft;
-            const uint32_t e = U(lut[tb + br.peek(LB)]);
-            uint32_t len = e >> 9;
-            sym = (e & 511u) - 1u;
-            if (e == 0) {  // longer than LB bits: bzip2's limit walk
-                const uint32_t t = tb >> LB;
-                uint32_t zn = LB + 1;
-                int32_t zvec = (int32_t)br.peek(zn);
-                while (zn <= kMaxLen && zvec > (int32_t)U((uint32_t)slimit[t][zn])) {
-                    ++zn;
-                    zvec = (int32_t)br.peek(zn);
-                }
-                const int idx = zvec - (int32_t)U((uint32_t)sbase[t][min(zn, (uint32_t)kMaxLen)]);
-                if (zn > kMaxLen || idx < 0 || idx >= alphaSize) {
-                    flag = kHost;
-                    zn = 1;
-                    sym = EOB;
-                } else {
-                    sym = U(sperm[t][idx]);
-                }
-                len = zn;
-            }
-            br.skip(len);
-            if (sym <= 1) {  // RUNA / RUNB: one digit of a run of the list front
-                es += (sym + 1) << rs;
-                flag |= ++rs > 21 ? kHost : 0u;
-            } else {
-                if (rs) {  // the run ends: es copies of the list front
-                    if (nblock + es > cap) flag = kHost;
-                    else {
-                        const uint32_t uc = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
-                        nblock += es;
-                        while (es) {
-                            if (op == 0 && es >= 64) {  // whole 64-byte pieces straight out
-                                const uint32_t whole = es & ~63u;
-                                const uint32_t at = nblock - es;
-                                for (uint32_t k = lane; k < whole; k += 64) ll[at + k] = (uint8_t)uc;
-                                es -= whole;
-                                continue;
-                            }
-                            const uint32_t take = min(es, 64u - op);
-                            obuf = lane - op < take ? uc : obuf;
-                            op += take;
-                            es -= take;
-                            if (op == 64) {
-                                ll[nblock - es - 64 + lane] = (uint8_t)obuf;
-                                op = 0;
-                            }
-                        }
+        uint32_t rs = 0;       // digits of a run still open at the end of the previous group
+        uint32_t g = 0;
+        bool eob = false;
+        while (!eob) {
+            if (g >= nSel || br.over()) { flag = kHost; break; }
+            const uint32_t tb = ((U(sel[g >> 3]) >> (4 * (g & 7))) & 15u) << LB;
+            ++g;
+            // 1. Huffman: symbol k of the group into lane k
+            uint32_t symv = 0, G = 0;
+            do {
+                const uint32_t e = U(lut[tb + br.peek(LB)]);
+                uint32_t len = e >> 9;
+                uint32_t sym = (e & 511u) - 1u;
+                if (e == 0) {  // longer than LB bits: bzip2's limit walk
+                    const uint32_t t = tb >> LB;
+                    uint32_t zn = LB + 1;
+                    int32_t zvec = (int32_t)br.peek(zn);
+                    while (zn <= kMaxLen && zvec > (int32_t)U((uint32_t)slimit[t][zn])) {
+                        ++zn;
+                        zvec = (int32_t)br.peek(zn);
                     }
-                    es = 0;
-                    rs = 0;
-                }
-                if (sym != EOB) {
-                    if (nblock >= cap) flag = kHost;
-                    else {
-                        const uint32_t nn = sym - 1;
-                        const uint32_t v =
-                            ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)((nn >> 2) & 63u)) >> (8 * (nn & 3))) & 0xFFu;
-                        // move to front: entries 0 .. nn shift up by one, v goes to 0
-                        // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
-                        const uint32_t up =
-                            (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
-                        const uint32_t sh = (mtfw << 8) | (up >> 24);
-                        const int k = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
-                        const uint32_t msk = k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
-                        mtfw = (sh & msk) | (mtfw & ~msk);
-                        // obuf[lane op] = v (v and op are wave-uniform)
-                        // (lane select in m0: one SGPR read per VALU op on this chip)
-                        asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(obuf) : "s"(v), "s"(op) : "m0");
-                        ++nblock;
-                        if (++op == 64) {
-                            ll[nblock - 64 + lane] = (uint8_t)obuf;
-                            op = 0;
-                        }
+                    const int idx = zvec - (int32_t)U((uint32_t)sbase[t][min(zn, (uint32_t)kMaxLen)]);
+                    if (zn > kMaxLen || idx < 0 || idx >= alphaSize) {
+                        flag = kHost;
+                        zn = 1;
+                        sym = EOB;
+                    } else {
+                        sym = U(sperm[t][idx]);
                     }
+                    len = zn;
                 }
+                br.skip(len);
+                // symv[lane G] = sym (sym and G are wave-uniform; lane select in m0)
+                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(symv) : "s"(sym), "s"(G) : "m0");
+                ++G;
+                eob = sym == EOB;
+            } while (G < 50 && !eob);
+            if (flag) break;
+            // 2. runs and counts over the lanes
+            const bool valid = lane < G;
+            const bool isrun = valid && symv <= 1u;
+            const bool isnorm = valid && symv > 1u && symv != EOB;
+            const uint64_t below = ~__ballot(isrun) & ltmask;   // non-run lanes before this one
+            const int p = 63 - (int)__clzll(below);             // the last of them, -1: none
+            const uint32_t j = (uint32_t)((int)lane - p - 1) + (p < 0 ? rs : 0u);  // digit index in its run
+            if (__ballot(isrun && j >= 21)) { flag = kHost; break; }  // run of 2^21 or more (decompress.c)
+            const uint32_t cnt = isrun ? (symv + 1u) << j : (isnorm ? 1u : 0u);
+            // the move-to-front chain over the group's ordinary symbols
+            const uint32_t front0 = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
+            uint32_t outb = 0;
+            for (uint64_t nm = __ballot(isnorm); nm; nm &= nm - 1) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(nm);
+                const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)symv, (int)k) - 1u;
+                const uint32_t v =
+                    ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)((nn >> 2) & 63u)) >> (8 * (nn & 3))) & 0xFFu;
+                // move to front: entries 0 .. nn shift up by one, v goes to 0
+                // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
+                const uint32_t up =
+                    (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
+                const uint32_t sh = (mtfw << 8) | (up >> 24);
+                const int kq = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
+                const uint32_t msk = kq >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kq)) - 1u);
+                mtfw = (sh & msk) | (mtfw & ~msk);
+                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(outb) : "s"(v), "s"(k) : "m0");
             }
-        } while (!flag && sym != EOB);
+            // a run repeats the list front: the byte of the last ordinary symbol before it
+            const uint32_t fb = (uint32_t)__shfl((int)outb, max(p, 0));
+            const uint32_t b = isrun ? (p < 0 ? front0 : fb) : outb;
+            // 3. offsets (exclusive prefix sum of the counts) and the stores
+            uint32_t incl = cnt;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+                if ((int)lane >= d) incl += o;
+            }
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            if (nblock + total > cap) { flag = kHost; break; }
+            const uint32_t at = nblock + incl - cnt;
+            if (isnorm || (isrun && cnt <= 8u))
+                for (uint32_t q = 0; q < cnt; ++q) ll[at + q] = (uint8_t)b;
+            for (uint64_t big = __ballot(isrun && cnt > 8u); big; big &= big - 1) {  // long stretches: all lanes
+                const int k = __builtin_ctzll(big);
+                const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)at, k);
+                const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, k);
+                const uint8_t bb = (uint8_t)__builtin_amdgcn_readlane((int)b, k);
+                for (uint32_t q = lane; q < c; q += 64) ll[o + q] = bb;
+            }
+            nblock += total;
+            rs = (uint32_t)__builtin_amdgcn_readlane((int)(isrun ? j + 1u : 0u), (int)(G - 1));
+        }
         if (flag) break;
-        if (lane < op) ll[nblock - op + lane] = (uint8_t)obuf;
         if (origPtr >= nblock || nblock == 0) { flag = kHost; break; }
         // end of stream: exactly one block
         const uint32_t e1 = br.get(24), e2 = br.get(24);
