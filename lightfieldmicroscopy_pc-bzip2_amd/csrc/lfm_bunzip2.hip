@@ -316,14 +316,14 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                 }
             }
             __syncthreads();
-            // lookup table: entry = sym + 1 (0: longer code) | length << 9
+            // lookup table: entry = sym | length << 9 (length 0: a longer code)
             uint16_t* lt = lut + (t << LB);
             for (int e = lane; e < (1 << LB); e += 64) {
                 uint16_t ent = 0;
                 for (int l = mn; l <= min(mx, LB); ++l) {
                     const int c = e >> (LB - l);  // the first l bits of e
                     if (c <= slimit[t][l] && c > slimit[t][l] - scnt[l]) {
-                        ent = (uint16_t)((sperm[t][c - sbase[t][l]] + 1) | (l << 9));
+                        ent = (uint16_t)(sperm[t][c - sbase[t][l]] | (l << 9));
                         break;
                     }
                 }
@@ -346,12 +346,11 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             const uint32_t tb = ((U(sel[g >> 3]) >> (4 * (g & 7))) & 15u) << LB;
             ++g;
             // 1. Huffman: symbol k of the group into lane k
-            uint32_t symv = 0, G = 0;
-            do {
+            auto decode1 = [&]() -> uint32_t {
                 const uint32_t e = U(lut[tb + br.peek(LB)]);
                 uint32_t len = e >> 9;
-                uint32_t sym = (e & 511u) - 1u;
-                if (e == 0) {  // longer than LB bits: bzip2's limit walk
+                uint32_t sym = e & 511u;
+                if (len == 0) {  // longer than LB bits: bzip2's limit walk
                     const uint32_t t = tb >> LB;
                     uint32_t zn = LB + 1;
                     int32_t zvec = (int32_t)br.peek(zn);
@@ -370,11 +369,25 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                     len = zn;
                 }
                 br.skip(len);
-                // symv[lane G] = sym (sym and G are wave-uniform; lane select in m0)
-                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(symv) : "s"(sym), "s"(G) : "m0");
-                ++G;
-                eob = sym == EOB;
-            } while (G < 50 && !eob);
+                return sym;
+            };
+            // symv[lane G] = sym (sym and G are wave-uniform; lane select in m0)
+            auto put = [](uint32_t& v, uint32_t sym, uint32_t G) {
+                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(sym), "s"(G) : "m0");
+            };
+            uint32_t symv = 0, G = 0;
+            if (g < nSel) {  // not the last group: 50 symbols, none of them EOB (libbzip2 writes
+                             // one selector per group, EOB in the last; anything else -> host)
+                for (G = 0; G < 50; ++G) put(symv, decode1(), G);
+                if (__ballot(lane < 50 && symv == EOB)) flag = kHost;
+            } else {
+                do {
+                    const uint32_t sym = decode1();
+                    put(symv, sym, G);
+                    ++G;
+                    eob = sym == EOB;
+                } while (G < 50 && !eob);
+            }
             if (flag) break;
             // 2. runs and counts over the lanes
             const bool valid = lane < G;
@@ -388,8 +401,9 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             // the move-to-front chain over the group's ordinary symbols
             const uint32_t front0 = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
             uint32_t outb = 0;
-            for (uint64_t nm = __ballot(isnorm); nm; nm &= nm - 1) {
+            for (uint64_t nm = __ballot(isnorm); nm;) {
                 const uint32_t k = (uint32_t)__builtin_ctzll(nm);
+                nm &= ~(1ull << k);
                 const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)symv, (int)k) - 1u;
                 const uint32_t v =
                     ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)((nn >> 2) & 63u)) >> (8 * (nn & 3))) & 0xFFu;
