@@ -371,12 +371,21 @@ def main():
         shm.close()
     if rank == 0 and world == 1 and not args.no_decode:
         buf = bytes(b)
-        t1 = time.perf_counter()
-        img = lfm.decode(buf, num_threads=threads)
-        dms = (time.perf_counter() - t1) * 1e3
         ref = d_img.cpu().numpy().view(np.uint16)
+        # three decodes, each into a fresh array (its first-touch page faults
+        # timed): the first also pays one-time costs (lazily loaded kernels,
+        # the decoder's device buffers and pinned staging); "ms" is the median
+        dlist, exact = [], True
+        for _ in range(3):
+            t1 = time.perf_counter()
+            img = lfm.decode(buf, num_threads=threads)
+            dlist.append((time.perf_counter() - t1) * 1e3)
+            exact = exact and bool(np.array_equal(img.reshape(ref.shape), ref))
+            del img
+        dms = float(np.median(dlist))
         line["decode"] = {"ms": round(dms, 1), "Mpixel_per_s": round(px_rank / dms / 1e3, 1),
-                          "exact": bool(np.array_equal(img.reshape(ref.shape), ref)),
+                          "first_ms": round(dlist[0], 1), "runs_ms": [round(x, 1) for x in dlist],
+                          "exact": exact,
                           "path": "GPU bzip2 decode + GPU inverse predictor (host libbz2 only for flagged streams, %d threads)" % threads}
     if rank == 0 and world == 1 and not args.no_host_input:
         line["host_input"] = host_input_rates(enc, d_img, zf)

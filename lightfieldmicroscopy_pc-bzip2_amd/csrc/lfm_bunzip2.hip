@@ -981,6 +981,37 @@ __global__ __launch_bounds__(256) void scatter_blocks(const uint8_t* __restrict_
     }
 }
 
+// the same with 16-byte copies: rows of a multiple of 16 bytes, 16-byte
+// aligned in both the block buffer and the image (checked by the launcher);
+// thread t of the grid's x dimension takes 16-byte units t, t + stride, ...
+// of the block's rows
+__global__ __launch_bounds__(256) void scatter_blocks16(const uint8_t* __restrict__ blocks, uint32_t stride, Grid5 G,
+                                                        uint32_t first, uint8_t* __restrict__ img)
+{
+    const uint32_t s = blockIdx.y;
+    uint32_t org[5], sz[5], id = first + s;
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+        const uint32_t q = id % G.nb[d];
+        id /= G.nb[d];
+        org[d] = q * G.bs[d];
+        sz[d] = min(G.bs[d], G.dims[d] - org[d]);
+    }
+    const uint32_t upr = sz[0] * G.bpp / 16;  // units per row
+    const uint32_t nu = upr * sz[1] * sz[2] * sz[3] * sz[4];
+    const uint4* src = (const uint4*)(blocks + (size_t)s * stride);
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += gridDim.x * blockDim.x) {
+        uint32_t q = u / upr;
+        const uint32_t c = u - q * upr;
+        const uint32_t y = q % sz[1]; q /= sz[1];
+        const uint32_t z = q % sz[2]; q /= sz[2];
+        const uint32_t cc = q % sz[3]; q /= sz[3];
+        const size_t dst = ((((size_t)(org[4] + q) * G.dims[3] + (org[3] + cc)) * G.dims[2] + (org[2] + z)) *
+                                G.dims[1] + (org[1] + y)) * G.dims[0] + org[0];
+        *((uint4*)(img + dst * G.bpp) + c) = src[u];
+    }
+}
+
 } // namespace bzd
 } // namespace lfm
 
@@ -997,7 +1028,16 @@ extern "C" int lfm_hip_scatter_blocks(const void* d_blocks, uint32_t stride, uin
         G.nb[d] = (dims[d] + bs[d] - 1) / bs[d];
     }
     G.bpp = bpp;
-    hipLaunchKernelGGL(lfm::bzd::scatter_blocks, dim3(64, count), dim3(256), 0, (hipStream_t)stream_,
-                       (const uint8_t*)d_blocks, stride, G, first, (uint8_t*)d_img);
+    // 16-byte units when every row of every block is a whole number of aligned
+    // units on both sides (the last block of a ragged dimension included)
+    bool v16 = ((uintptr_t)d_blocks & 15) == 0 && ((uintptr_t)d_img & 15) == 0 && stride % 16 == 0 &&
+               ((size_t)dims[0] * bpp) % 16 == 0 && ((size_t)bs[0] * bpp) % 16 == 0;
+    if (v16 && dims[0] % bs[0]) v16 = ((size_t)(dims[0] % bs[0]) * bpp) % 16 == 0;
+    if (v16)
+        hipLaunchKernelGGL(lfm::bzd::scatter_blocks16, dim3(8, count), dim3(256), 0, (hipStream_t)stream_,
+                           (const uint8_t*)d_blocks, stride, G, first, (uint8_t*)d_img);
+    else
+        hipLaunchKernelGGL(lfm::bzd::scatter_blocks, dim3(64, count), dim3(256), 0, (hipStream_t)stream_,
+                           (const uint8_t*)d_blocks, stride, G, first, (uint8_t*)d_img);
     return hipGetLastError() == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
 }
