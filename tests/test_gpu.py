@@ -446,6 +446,25 @@ def test_decode_roundtrip_through_gpu(lfmlib, oracle, gpu, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(200, 136, 20), (256, 96, 16), (96, 96, 9)])
+def test_decode_multilayer_roundtrip(lfmlib, oracle, gpu, tmp_path, shape):
+    """Stacks of several block layers along z (ragged x / y blocks, an odd
+    number of layers, a last layer of one frame) round-trip through the GPU
+    writer and reader."""
+    X, Y, Z = shape
+    img = oracle.synthetic_lf(X, Y, Z=Z, T=13, seed=X + Z)
+    for fam, hv in (("angle", 0), ("tiles", 8 + 2)):
+        lfmlib.set_family(fam)
+        try:
+            p = tmp_path / ("layers_%s.lfm" % fam)
+            lfmlib.write_lfm(str(p), img, predictor_request=hv & 0x7F, nnum=13, video=0)
+            out, _, _ = lfmlib.read_lfm(str(p))
+        finally:
+            lfmlib.set_family("tiles")
+        assert np.array_equal(out, img), (fam, shape)
+
+
+@pytest.mark.gpu
 def test_decode_roundtrip_5d_through_gpu(lfmlib, oracle, gpu, tmp_path):
     """5-D stacks (c, t > 1: one predictor volume per (c, t)) with small blocks
     round-trip through the GPU writer and reader (pipelined inverse predictor,
