@@ -256,7 +256,6 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
     __shared__ uint8_t tout[kRleTile + kRleTile / 4 + 64];
     __shared__ RunSum wrs[NW];
     __shared__ uint32_t wcnt[NW], wcrc[NW];
-    __shared__ uint32_t inuse[8];
     __shared__ RunSum s_carry;
     __shared__ uint32_t s_wr, s_crc;
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -280,26 +279,36 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
     };
     for (uint32_t i = t; i < 1024; i += kRleThreads) crc4[i >> 8][i & 255] = c_crc4[i >> 8][i & 255];
-    if (t < 8) inuse[t] = 0;
     if (t == 0) {
         s_carry = RunSum{0, 0, 0, 0, 0};
         s_wr = 0;
         s_crc = 0;
     }
-    uint32_t pm[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // bytes present
     uint8_t* Tout = B.T + (size_t)s * B.cap;
     const uint32_t wlim = B.cap - 8;  // RLE1 bytes past this are not stored (the stream goes to the host)
+    // this thread's 32 bytes of a tile; the next tile's are loaded while this
+    // one is processed
+    auto load_chunk = [&](uint32_t g, uint32_t nv, uint4& a, uint4& b) {
+        a = make_uint4(0, 0, 0, 0);
+        b = make_uint4(0, 0, 0, 0);
+        if (nv) a = load16(g);
+        if (nv > 16) b = load16(g + 16);
+    };
+    uint4 na, nb;
+    {
+        const uint32_t g = t * kRleChunk;
+        load_chunk(g, g < L ? min(kRleChunk, L - g) : 0u, na, nb);
+    }
     __syncthreads();
     for (uint32_t tb = 0; tb < L; tb += kRleTile) {
         const uint32_t g = tb + t * kRleChunk;
         const uint32_t nv = g < L ? min(kRleChunk, L - g) : 0u;
         uint32_t w[8];
+        w[0] = na.x; w[1] = na.y; w[2] = na.z; w[3] = na.w;
+        w[4] = nb.x; w[5] = nb.y; w[6] = nb.z; w[7] = nb.w;
         {
-            uint4 a = make_uint4(0, 0, 0, 0), b = make_uint4(0, 0, 0, 0);
-            if (nv) a = load16(g);
-            if (nv > 16) b = load16(g + 16);
-            w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
-            w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+            const uint32_t g2 = g + kRleTile;
+            load_chunk(g2, g2 < L ? min(kRleChunk, L - g2) : 0u, na, nb);
         }
         if (nv < kRleChunk) {  // zero padding past L
 #pragma unroll
@@ -315,7 +324,7 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t x = cc ^ __builtin_bswap32(w[q]);
             cc = crc4[3][x >> 24] ^ crc4[2][(x >> 16) & 255u] ^ crc4[1][(x >> 8) & 255u] ^ crc4[0][x & 255u];
         }
-        // chunk run summary and byte presence
+        // chunk run summary
         RunSum rs{nv, w[0] & 255u, 0, 0, 0};
         {
             uint32_t prev = 256, lead = 0, trail = 0;
@@ -330,9 +339,6 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
                     }
                     trail = c == prev ? trail + 1 : 1;
                     prev = c;
-                    const uint32_t bit = 1u << (c & 31), wi = c >> 5;
-#pragma unroll
-                    for (uint32_t k = 0; k < 8; ++k) pm[k] |= wi == k ? bit : 0u;
                 }
             }
             rs.last = prev;
@@ -378,14 +384,7 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (has_end) emit(ch, rl);  // flush_RL of the final run
         };
         uint32_t cnt = 0;
-        walk([&](uint32_t c, uint32_t l) {
-            if (l >= 4) {
-                atomicOr(&inuse[(l - 4) >> 5], 1u << ((l - 4) & 31));
-                cnt += 5;
-            } else {
-                cnt += l;
-            }
-        });
+        walk([&](uint32_t, uint32_t l) { cnt += l >= 4 ? 5u : l; });
         uint32_t cinc = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -440,13 +439,6 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             s_wr = wr0 + total;
         }
     }
-    // byte presence: OR over the wave, then into the LDS map
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-        uint32_t v = pm[k];
-        for (int d = 32; d > 0; d >>= 1) v |= __shfl_xor(v, d);
-        if (lane == 0 && v) atomicOr(&inuse[k], v);
-    }
     __syncthreads();
     if (t == 0) {
         const uint32_t total = s_wr;
@@ -462,7 +454,8 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
         B.seg_begin[s] = s * B.cap;
         B.seg_end[s] = s * B.cap + (host ? 0u : total);
     }
-    if (t < 8) B.inuse[s * 8 + t] = inuse[t];
+    // the byte map of the RLE1 text comes from bwt_bucket's histogram
+    if (t < 8) B.inuse[s * 8 + t] = 0u;
 }
 
 // ------------------------------------------------------------------ BWT --
@@ -542,6 +535,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
     __shared__ uint32_t ccount[3], cbase[3];
+    __shared__ uint32_t sinuse[8];  // bytes present in the RLE1 text (the stream's inUse map)
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
@@ -552,6 +546,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
     for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
     if (t < 3) ccount[t] = 0;
+    if (t < 8) sinuse[t] = 0;
     // histogram of the BITS-bit bucket
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
         const uint32_t m = bucket_tile(T, n, i0, tile);
@@ -561,8 +556,13 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     }
     // exclusive scan of the buckets; chunk cuts at bucket ends
     constexpr uint32_t per = kBuckets / kBucketThreads;
+    static_assert(per <= (1u << (BITS - 8)), "a thread's buckets share their first byte");
     uint32_t sum = 0;
     for (uint32_t q = 0; q < per; ++q) sum += hist[t * per + q];
+    if (sum) {  // every byte of the text starts a rotation: byte c is present iff its buckets are not empty
+        const uint32_t c = (t * per) >> (BITS - 8);
+        atomicOr(&sinuse[c >> 5], 1u << (c & 31));
+    }
     uint32_t isum = sum;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t a = __shfl_up(isum, d);
@@ -612,6 +612,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
             ++at;
         });
     }
+    if (t < 8) B.inuse[s * 8 + t] = sinuse[t];  // (written after the scan's barrier)
     // bucket starts for the scatter
     {
         uint32_t off = my0;
