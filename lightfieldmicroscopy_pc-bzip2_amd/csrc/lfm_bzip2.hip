@@ -1431,13 +1431,12 @@ constexpr uint32_t kRle2Tile = kRle2Threads * kRle2Per;  // 16384
 // with coalesced stores; the run pending at the tile end carries over.
 __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
 {
-    __shared__ uint32_t counts[kRle2Threads];
-    __shared__ uint32_t zsum[kRle2Threads];   // trailing zeros of the prefix (scan)
-    __shared__ uint32_t allz[kRle2Threads];   // prefix entirely zeros
+    constexpr uint32_t NW = kRle2Threads / 64;
+    __shared__ uint32_t wz[NW], wa[NW], wc[NW];  // per-wave scan totals
     __shared__ uint32_t freq[kMaxAlpha];
     __shared__ uint16_t tile_out[kRle2Tile + 64];
     __shared__ uint32_t s_carry, s_wr;
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
     const size_t o = (size_t)s * B.cap;
@@ -1451,40 +1450,58 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         s_carry = 0;
         s_wr = 0;
     }
+    uint32_t nrun[2] = {0, 0};  // RUNA / RUNB, the hottest symbols, counted here
+    // zero-run scan element: (trailing zeros, all zeros); a then b
+    auto zcomb = [](uint32_t atz, uint32_t aaz, uint32_t btz, uint32_t baz, uint32_t& rtz, uint32_t& raz) {
+        rtz = baz ? atz + btz : btz;
+        raz = aaz & baz;
+    };
     __syncthreads();
     for (uint32_t tb = 0; tb < n; tb += kRle2Tile) {
-        const uint32_t c0 = min(n, tb + t * kRle2Per), c1 = min(n, c0 + kRle2Per);
+        const uint32_t c0 = min(n, tb + t * kRle2Per), c1 = min(n, c0 + kRle2Per), len = c1 - c0;
         const bool last_tile = tb + kRle2Tile >= n;
-        // chunk summary: trailing zeros, all-zero
-        uint32_t tz = 0;
-        bool az = true;
-        for_bytes(m + c0, c1 - c0, [&](uint32_t v) {
+        // this thread's values, once, in registers
+        uint32_t q[kRle2Per / 4];
+#pragma unroll
+        for (uint32_t i = 0; i < kRle2Per / 16; ++i) {
+            const uint4 v = 16 * i < len ? *(const uint4*)(m + c0 + 16 * i) : make_uint4(0, 0, 0, 0);
+            q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+        }
+        auto each = [&](auto&& f) {
+#pragma unroll
+            for (uint32_t i = 0; i < kRle2Per; ++i)
+                if (i < len) f((q[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+        };
+        // chunk summary: trailing zeros, all-zero (empty chunks pass the carry through)
+        uint32_t tz = 0, az = 1;
+        each([&](uint32_t v) {
             if (v == 0) ++tz;
-            else { tz = 0; az = false; }
+            else { tz = 0; az = 0; }
         });
-        zsum[t] = tz;
-        allz[t] = (c1 > c0) ? (az ? 1u : 0u) : 1u;  // empty chunks pass the carry through
+        // inclusive scan over the wave, then the waves before
+        uint32_t itz = tz, iaz = az;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t otz = (uint32_t)__shfl_up((int)itz, d), oaz = (uint32_t)__shfl_up((int)iaz, d);
+            if ((int)lane >= d) zcomb(otz, oaz, itz, iaz, itz, iaz);
+        }
+        if (lane == 63) {
+            wz[wave] = itz;
+            wa[wave] = iaz;
+        }
         const uint32_t tile_carry = s_carry;
         __syncthreads();
-        for (uint32_t off = 1; off < kRle2Threads; off <<= 1) {
-            uint32_t at = 0, aa = 1;
-            if (t >= off) { at = zsum[t - off]; aa = allz[t - off]; }
-            const uint32_t bt = zsum[t], ba = allz[t];
-            __syncthreads();
-            if (t >= off) {
-                zsum[t] = ba ? at + bt : bt;
-                allz[t] = ba & aa;
-            }
-            __syncthreads();
-        }
-        // zeros pending at the chunk start: the previous threads' trailing run,
-        // extended by the tile carry when everything before is zeros
-        const uint32_t carry = t ? (allz[t - 1] ? tile_carry + zsum[t - 1] : zsum[t - 1]) : tile_carry;
-        const uint32_t tile_end_zeros = allz[kRle2Threads - 1] ? tile_carry + zsum[kRle2Threads - 1]
-                                                               : zsum[kRle2Threads - 1];
-        const bool has_last = last_tile && c0 < c1 && c1 == n;
+        uint32_t ptz = tile_carry, paz = 1;  // everything before the wave, the tile carry first
+        for (uint32_t w2 = 0; w2 < wave; ++w2) zcomb(ptz, paz, wz[w2], wa[w2], ptz, paz);
+        uint32_t etz = (uint32_t)__shfl_up((int)itz, 1), eaz = (uint32_t)__shfl_up((int)iaz, 1);
+        if (lane == 0) { etz = 0; eaz = 1; }
+        uint32_t carry, cz;  // zeros pending at the chunk start
+        zcomb(ptz, paz, etz, eaz, carry, cz);
+        uint32_t tile_end_zeros = tile_carry, tez = 1;
+        for (uint32_t w2 = 0; w2 < NW; ++w2) zcomb(tile_end_zeros, tez, wz[w2], wa[w2], tile_end_zeros, tez);
+        const bool has_last = last_tile && len && c1 == n;
         uint32_t z = carry, w = 0;
-        for_bytes(m + c0, c1 - c0, [&](uint32_t v) {
+        each([&](uint32_t v) {
             if (v == 0) { ++z; return; }
             if (z) { w += run_digits(z); z = 0; }
             ++w;
@@ -1493,19 +1510,24 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
             if (z) w += run_digits(z);
             ++w;  // EOB
         }
-        counts[t] = w;
-        __syncthreads();
-        for (uint32_t off = 1; off < kRle2Threads; off <<= 1) {
-            const uint32_t v = t >= off ? counts[t - off] : 0u;
-            __syncthreads();
-            counts[t] += v;
-            __syncthreads();
+        // output offsets: scan of the counts
+        uint32_t ic = w;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t oc = (uint32_t)__shfl_up((int)ic, d);
+            if ((int)lane >= d) ic += oc;
         }
-        uint32_t wr = counts[t] - w;
-        const uint32_t tile_total = counts[kRle2Threads - 1];
+        if (lane == 63) wc[wave] = ic;
+        __syncthreads();
+        uint32_t wr = ic - w, tile_total = 0;
+        for (uint32_t w2 = 0; w2 < NW; ++w2) {
+            if (w2 < wave) wr += wc[w2];
+            tile_total += wc[w2];
+        }
         auto emit = [&](uint32_t v) {
             tile_out[wr++] = (uint16_t)v;
-            atomicAdd(&freq[v], 1u);
+            if (v < 2) ++nrun[v];
+            else atomicAdd(&freq[v], 1u);
         };
         auto zeros = [&](uint32_t zz) {
             uint32_t zp = zz - 1;
@@ -1516,7 +1538,7 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
             }
         };
         z = carry;
-        for_bytes(m + c0, c1 - c0, [&](uint32_t v) {
+        each([&](uint32_t v) {
             if (v == 0) { ++z; return; }
             if (z) { zeros(z); z = 0; }
             emit(v + 1);
@@ -1535,6 +1557,14 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         }
         __syncthreads();
     }
+    static_assert(kRunA == 0 && kRunB == 1, "RUNA / RUNB are symbols 0 and 1");
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        uint32_t c = nrun[r];
+        for (int d = 32; d > 0; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d);
+        if (lane == 0 && c) atomicAdd(&freq[r], c);
+    }
+    __syncthreads();
     if (t == 0) {
         B.nmtf[s] = s_wr;
         if (!heap_narrow(B, s, (int)nin + 2)) B.wide[atomicAdd(B.wide_cnt, 1u)] = s;  // u64 Huffman heaps
