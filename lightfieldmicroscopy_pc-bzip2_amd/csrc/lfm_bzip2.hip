@@ -1297,6 +1297,29 @@ __device__ __forceinline__ void wsync()
 
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
 
+// exclusive prefix OR of a 64-bit value over the wave's lanes with DPP row
+// shifts and row broadcasts (VALU only: the ds_bpermute shuffles it replaces
+// were a chain of 14 LDS round trips per 64-position window)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_get(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_or_scan_excl32(uint32_t x)
+{
+    x |= dpp_get<0x111, 0xF>(x);  // row_shr:1
+    x |= dpp_get<0x112, 0xF>(x);  // row_shr:2
+    x |= dpp_get<0x114, 0xF>(x);  // row_shr:4
+    x |= dpp_get<0x118, 0xF>(x);  // row_shr:8
+    x |= dpp_get<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+    x |= dpp_get<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+    return dpp_get<0x138, 0xF>(x);  // wave_shr:1: exclusive
+}
+__device__ __forceinline__ uint64_t wave_or_scan_excl(uint64_t x)
+{
+    return ((uint64_t)wave_or_scan_excl32((uint32_t)(x >> 32)) << 32) | wave_or_scan_excl32((uint32_t)x);
+}
+
 __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const int32_t* __restrict__ seg_last)
 {
     __shared__ int32_t key[4][256];
@@ -1347,13 +1370,7 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
         const uint32_t p_in = has_prev ? 63u - (uint32_t)__clzll(before) : 0u;
         const uint32_t P0 = Pt[wave][c];
         // U = OR over lanes k < lane of bit(prev_k)  (exclusive prefix OR)
-        uint64_t U = has_prev ? (1ull << p_in) : 0ull;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t t = __shfl_up(U, d);
-            if ((int)lane >= d) U |= t;
-        }
-        U = __shfl_up(U, 1);
-        if (lane == 0) U = 0ull;
+        const uint64_t U = wave_or_scan_excl(has_prev ? (1ull << p_in) : 0ull);
         uint32_t m;
         if (has_prev) {
             m = (uint32_t)__popcll((lt & ~U) >> (p_in + 1));
