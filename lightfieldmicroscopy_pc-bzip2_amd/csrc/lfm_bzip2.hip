@@ -495,11 +495,15 @@ constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
 constexpr uint32_t kSmallCap = kCsThreads * kCsItems, kBigCap = kBigThreads * kBigItems;
 constexpr uint32_t kMaxCuts = 1024;                // >= 3 * cap / kChunk + 2
 
-// chunk lists: [0] <= kSmallCap, [1] <= kBigCap, [2] larger (rocPRIM)
+// chunk lists: [3] <= kTinyCap, [0] <= kSmallCap, [1] <= kBigCap, [2] larger
+// (rocPRIM segmented sort)
+constexpr uint32_t kTinyCap = 1024;  // half-size sorter: the ~40 % of chunks at most
+                                     // this long would pad a kSmallCap sort to twice their size
 struct ChunkLists {
-    uint32_t* b[3];
-    uint32_t* e[3];
-    uint32_t* cnt;   // 3 counters
+    uint32_t* b[4];
+    uint32_t* e[4];
+    uint32_t* cnt;   // counters of classes 0..2
+    uint32_t* cnt3;  // counter of class 3
 };
 
 // stage T[i0 - 1 .. i0 + m + 8) cyclically into tile[0 .. m + 9), m = min(n - i0, kBktTile)
@@ -534,7 +538,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     __shared__ uint8_t tile[kBktTile + 16];
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
-    __shared__ uint32_t ccount[3], cbase[3];
+    __shared__ uint32_t ccount[4], cbase[4];
     __shared__ uint32_t sinuse[8];  // bytes present in the RLE1 text (the stream's inUse map)
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
@@ -545,7 +549,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     // see up to 15 bytes past n, which must read as "not tied"
     if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
     for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
-    if (t < 3) ccount[t] = 0;
+    if (t < 4) ccount[t] = 0;
     if (t < 8) sinuse[t] = 0;
     // histogram of the BITS-bit bucket
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
@@ -630,12 +634,12 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         cb = t ? cuts[t - 1] : 0u;
         ce = t + 1 < nch ? cuts[t] : n;
         const uint32_t m = ce > cb ? ce - cb : 0u;
-        cls = m <= kSmallCap ? 0u : (m <= kBigCap ? 1u : 2u);
+        cls = m <= kTinyCap ? 3u : (m <= kSmallCap ? 0u : (m <= kBigCap ? 1u : 2u));
         if (m) slot = atomicAdd(&ccount[cls], 1u);
         else cb = ce;
     }
     __syncthreads();
-    if (t < 3) cbase[t] = ccount[t] ? atomicAdd(&L.cnt[t], ccount[t]) : 0u;
+    if (t < 4) cbase[t] = ccount[t] ? atomicAdd(t < 3 ? &L.cnt[t] : L.cnt3, ccount[t]) : 0u;
     __syncthreads();
     if (t < nch && ce > cb) {
         L.b[cls][cbase[cls] + slot] = o + cb;
@@ -2742,9 +2746,9 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         hipLaunchKernelGGL(rle1_crc<false>, dim3(count), dim3(kRleThreads), 0, st, B);
     }
     if (!ok()) return LFM_HIP_ERUNTIME;
-    // counters after offs: [0..2] chunk classes of the bucket pass, then the
-    // tied-list counts [0], [1]; [3] wide Huffman streams, [4] Huffman
-    // retries
+    // counters after offs: [0..2] chunk classes 0..2 of the bucket pass (then
+    // the tied-list counts [0], [1]); [3] wide Huffman streams, [4] Huffman
+    // retries, [5] chunk class 3
     uint32_t* d_cnt = (uint32_t*)(offs + count + 1);
     B.wide_cnt = d_cnt + 3;
     mark(1);
@@ -2752,12 +2756,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     {
         ChunkLists CL;
         const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
-        for (int c = 0; c < 3; ++c) {
+        for (int c = 0; c < 4; ++c) {
             CL.b[c] = B.cl0 + c * q;
             CL.e[c] = B.cl1 + c * q;
         }
         CL.cnt = d_cnt;
-        uint32_t nch[3] = {0, 0, 0};
+        CL.cnt3 = d_cnt + 5;
+        uint32_t nch[6] = {0, 0, 0, 0, 0, 0};
         if (hipMemsetAsync(d_cnt, 0, 32, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
@@ -2768,7 +2773,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         if (bkt_bits == 13) hipLaunchKernelGGL(bwt_bucket<13>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
         else if (bkt_bits == 15) hipLaunchKernelGGL(bwt_bucket<15>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
         else hipLaunchKernelGGL(bwt_bucket<14>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
-        if (!ok() || hipMemcpyAsync(nch, d_cnt, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        if (!ok() || hipMemcpyAsync(nch, d_cnt, 24, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         static const int cs_shape = std::getenv("LFM_CS_SHAPE") ? std::atoi(std::getenv("LFM_CS_SHAPE")) : 0;
@@ -2779,6 +2784,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             return dim3(cs_xcd ? 8 * per : nc);
         };
         uint32_t per = 0;
+        if (nch[5]) {
+            const dim3 g = cs_grid(nch[5], per);
+            hipLaunchKernelGGL((bwt_chunk_sort<kTinyCap / kCsItems, kCsItems>), g, dim3(kTinyCap / kCsItems), 0, st, B,
+                               CL.b[3], CL.e[3], nch[5], per);
+        }
         if (nch[0]) {
             const dim3 g = cs_grid(nch[0], per);
             if (cs_shape == 1)  // 1024 threads x 2 items (same capacity)
