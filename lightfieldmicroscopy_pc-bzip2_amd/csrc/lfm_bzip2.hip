@@ -506,26 +506,46 @@ struct ChunkLists {
     uint32_t* cnt3;  // counter of class 3
 };
 
-// stage T[i0 - 1 .. i0 + m + 8) cyclically into tile[0 .. m + 9), m = min(n - i0, kBktTile)
-__device__ __forceinline__ uint32_t bucket_tile(const uint8_t* __restrict__ T, uint32_t n, uint32_t i0, uint8_t* tile)
+// A tile of the text for the bucket pass: T[i0 - 1 .. i0 + m + 8) cyclically
+// in tile[0 .. m + 9), m = min(n - i0, kBktTile).  bucket_fetch loads this
+// thread's part (4 bytes; one edge byte for threads 0..8) into registers, a
+// tile ahead of bucket_put, which stores it into LDS: the pass is a chain of
+// tiles, and waiting for each tile's loads was most of its time.
+struct BktPart {
+    uint32_t w;
+    uint32_t e;
+};
+
+__device__ __forceinline__ BktPart bucket_fetch(const uint8_t* __restrict__ T, uint32_t n, uint32_t i0)
 {
+    BktPart p{0u, 0u};
+    if (i0 >= n) return p;
     const uint32_t t = threadIdx.x;
     const uint32_t m = min(n - i0, kBktTile);
-    if (4 * t < m) {  // may read up to 3 bytes past n: inside the stream's cap
-        const uint32_t w = *(const uint32_t*)(T + i0 + 4 * t);
-        tile[1 + 4 * t] = (uint8_t)w;
-        tile[2 + 4 * t] = (uint8_t)(w >> 8);
-        tile[3 + 4 * t] = (uint8_t)(w >> 16);
-        tile[4 + 4 * t] = (uint8_t)(w >> 24);
-    }
-    __syncthreads();
+    if (4 * t < m) p.w = *(const uint32_t*)(T + i0 + 4 * t);  // may read up to 3 bytes past n: inside the stream's cap
     if (t < 8) {
         uint32_t j = i0 + m + t;
         while (j >= n) j -= n;
-        tile[1 + m + t] = T[j];
+        p.e = T[j];
     } else if (t == 8) {
-        tile[0] = T[i0 ? i0 - 1 : n - 1];
+        p.e = T[i0 ? i0 - 1 : n - 1];
     }
+    return p;
+}
+
+__device__ __forceinline__ uint32_t bucket_put(const BktPart& p, uint32_t n, uint32_t i0, uint8_t* tile)
+{
+    const uint32_t t = threadIdx.x;
+    const uint32_t m = min(n - i0, kBktTile);
+    if (4 * t < m) {
+        tile[1 + 4 * t] = (uint8_t)p.w;
+        tile[2 + 4 * t] = (uint8_t)(p.w >> 8);
+        tile[3 + 4 * t] = (uint8_t)(p.w >> 16);
+        tile[4 + 4 * t] = (uint8_t)(p.w >> 24);
+    }
+    __syncthreads();  // the edge bytes overwrite the bytes read past the tile
+    if (t < 8) tile[1 + m + t] = (uint8_t)p.e;
+    else if (t == 8) tile[0] = (uint8_t)p.e;
     __syncthreads();
     return m;
 }
@@ -552,8 +572,11 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     if (t < 4) ccount[t] = 0;
     if (t < 8) sinuse[t] = 0;
     // histogram of the BITS-bit bucket
+    BktPart nx = bucket_fetch(T, n, 0);
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
-        const uint32_t m = bucket_tile(T, n, i0, tile);
+        const BktPart cur = nx;
+        nx = bucket_fetch(T, n, i0 + kBktTile);
+        const uint32_t m = bucket_put(cur, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads)
             atomicAdd(&hist[((uint32_t)tile[1 + k] << (BITS - 8)) | (tile[2 + k] >> (16 - BITS))], 1u);
         __syncthreads();
@@ -648,8 +671,11 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     // scatter of the values only (start | preceding byte << 24): the sorters
     // rebuild the 8-byte keys from the text (rot_key8_fast), which the L2s
     // hold, instead of 8-byte scattered key writes and their re-read
+    nx = bucket_fetch(T, n, 0);
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
-        const uint32_t m = bucket_tile(T, n, i0, tile);
+        const BktPart cur = nx;
+        nx = bucket_fetch(T, n, i0 + kBktTile);
+        const uint32_t m = bucket_put(cur, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads) {
             const uint8_t* p = tile + 1 + k;
             const uint32_t pos = atomicAdd(&hist[((uint32_t)p[0] << (BITS - 8)) | (p[1] >> (16 - BITS))], 1u);
