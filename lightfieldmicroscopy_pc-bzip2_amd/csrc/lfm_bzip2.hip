@@ -1164,7 +1164,11 @@ __global__ __launch_bounds__(256) void mtf_last(Batch B, uint32_t nseg_max, int3
         if ((v & kIdxMask) == 0) B.orig_ptr[s] = j;  // BZ2_blockSort: origPtr = sorted position of rotation 0
         const uint32_t ll = u2s[wave][v >> 24];
         llbuf[j] = (uint8_t)ll;
-        atomicMax(&last[wave][ll], (int32_t)j);
+        // only the last position of each run of equal symbols (the next lane
+        // holds position j + 1) can be the symbol's last: the BWT output is
+        // runs, and 64 lanes on one LDS word serialise
+        const uint32_t nxt = (uint32_t)__builtin_amdgcn_mov_dpp((int)ll, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        if (lane == 63 || j + 1 >= j1 || nxt != ll) atomicMax(&last[wave][ll], (int32_t)j);
     }
     __builtin_amdgcn_wave_barrier();
     int32_t* dst = seg_last + ((size_t)s * nseg_max + k) * 256;
