@@ -2263,9 +2263,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
 // The header: the fixed fields and the mapping table by one lane, then the
 // selectors (unary MTF values) and the delta-coded code lengths as items
 // written by all threads at prefix-summed bit offsets.
+constexpr uint32_t kEmitC = 16;  // symbols per thread and round
+constexpr uint32_t kEmitBufWords = (kEmitThreads * kEmitC * 17 + 31) / 32 + 2;  // code lengths <= 17 bits
+
 __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
 {
     __shared__ uint32_t wsum[kEmitThreads / 64];
+    __shared__ uint32_t obuf[kEmitBufWords];
     __shared__ uint64_t s_hdr_bits;
     __shared__ uint32_t hdr[kHdrWords];
     __shared__ uint32_t lc[kMaxGroups * kMaxAlpha];  // code | len << 24 per (table, symbol)
@@ -2388,77 +2392,85 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
         if (t == 0) s_hdr_bits = p;
     }
     __syncthreads();
-    // data bits: thread t codes symbols [i0, i1), read 8 at a time
-    const uint32_t per = ((nMTF + kEmitThreads - 1) / kEmitThreads + 7) & ~7u;
-    const uint32_t i0 = min(nMTF, t * per), i1 = min(nMTF, i0 + per);
+    // data bits, in rounds of kEmitC symbols per thread (thread t codes
+    // symbols r0 + t * kEmitC ..): a round's bits are contiguous across the
+    // threads, so they are assembled in LDS and leave in coalesced word
+    // stores; the round's partial last word carries into the next round.
+    // (Each thread writing its own stretch of the stream straight to memory
+    // made every store instruction touch 64 scattered lines.)
+    const uint64_t hb = s_hdr_bits;
+    {
+        // header words; the word holding the data's first bit starts the carry
+        const uint32_t full = (uint32_t)min<uint64_t>(hb >> 5, kHdrWords - 1);
+        for (uint32_t w = t; w < full; w += kEmitThreads) words[w] = hdr[w];
+        if (t == 0 && (hb >> 5) >= kHdrWords - 1) atomicOr(&words[kHdrWords - 1], hdr[kHdrWords - 1]);
+        for (uint32_t i = t; i < kEmitBufWords; i += kEmitThreads) obuf[i] = 0;
+    }
+    __syncthreads();
+    if (t == 0)  // a spilled header's last word is in memory (OR-ed there), else in LDS
+        obuf[0] = (hb >> 5) < kHdrWords - 1 ? hdr[hb >> 5] : atomicOr(&words[hb >> 5], 0u);
+    __syncthreads();
     auto sym_lc = [&](uint32_t i, uint32_t v) {
         const uint32_t g = i / kGSize;
         const uint32_t tb = g < kSelLds ? sel_l[g] : sel[g];
         return lc[tb * kMaxAlpha + v];
     };
-    auto for_syms = [&](auto&& f) {
-        for (uint32_t i = i0; i < i1; i += 8) {
-            const uint4 v = *(const uint4*)(mtfv + i);  // rows are 16-byte aligned, i0 a multiple of 8
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint64_t bitpos = hb;
+    for (uint32_t r0 = 0; r0 < nMTF; r0 += kEmitThreads * kEmitC) {
+        const uint32_t i0 = min(nMTF, r0 + t * kEmitC), i1 = min(nMTF, i0 + kEmitC);
+        uint32_t e[kEmitC];
+        uint32_t nb = 0;
+        {
+            const uint4 v0 = i0 < i1 ? *(const uint4*)(mtfv + i0) : make_uint4(0, 0, 0, 0);
+            const uint4 v1 = i0 + 8 < i1 ? *(const uint4*)(mtfv + i0 + 8) : make_uint4(0, 0, 0, 0);
+            const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k)
-                if (i + k < i1) f(i + k, (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-        }
-    };
-    uint32_t nb = 0;
-    for_syms([&](uint32_t i, uint32_t v) { nb += sym_lc(i, v) >> 24; });
-    uint32_t data_bits = 0;
-    const uint32_t excl = block_excl_scan<kEmitThreads>(nb, wsum, &data_bits);
-    const uint64_t data0 = s_hdr_bits;
-    const uint64_t my0 = data0 + excl;
-    const uint64_t data_end = data0 + data_bits;
-    const uint64_t hb = data0;
-    {
-        // zero the words that are OR-ed into: each thread's edge words, the end
-        // marker's; a spilled header's last word already holds header bits
-        auto zero = [&](uint64_t w) {
-            if (!(w == (hb >> 5) && (hb >> 5) >= kHdrWords - 1)) words[w] = 0;
-        };
-        if (nb) {
-            zero(my0 >> 5);
-            zero((my0 + nb - 1) >> 5);
-        }
-        if (t == 0)
-            for (uint64_t w = data_end >> 5; w <= ((data_end + 80) >> 5) + 1; ++w) zero(w);
-    }
-    __syncthreads();
-    {
-        // full header words are the header's alone; the partial last one is
-        // shared with the first symbols (atomicOr)
-        const uint32_t full = (uint32_t)min<uint64_t>(hb >> 5, kHdrWords - 1);
-        for (uint32_t w = t; w < full; w += kEmitThreads) words[w] = hdr[w];
-        if (t == 0 && (hb >> 5) < kHdrWords - 1 && (hb & 31)) atomicOr(&words[hb >> 5], hdr[hb >> 5]);
-        if (t == 0 && (hb >> 5) >= kHdrWords - 1) atomicOr(&words[kHdrWords - 1], hdr[kHdrWords - 1]);
-    }
-    if (i1 > i0) {
-        // accumulate whole words locally; only the two edge words are shared
-        uint64_t acc = 0;  // pending bits, left aligned at bit 63
-        uint32_t wpos = (uint32_t)(my0 >> 5);
-        uint32_t nacc = (uint32_t)(my0 & 31);  // the first word starts that many bits in (others' bits)
-        bool first_word = true;
-        for_syms([&](uint32_t i, uint32_t v) {
-            const uint32_t e = sym_lc(i, v);
-            const uint32_t l = e >> 24;
-            acc |= ((uint64_t)(e & 0xFFFFFFu) << (64 - l)) >> nacc;
-            nacc += l;
-            if (nacc >= 32) {
-                const uint32_t w = (uint32_t)(acc >> 32);
-                if (first_word) atomicOr(&words[wpos], w);
-                else words[wpos] = w;
-                first_word = false;
-                ++wpos;
-                acc <<= 32;
-                nacc -= 32;
+            for (uint32_t k = 0; k < kEmitC; ++k) {
+                e[k] = i0 + k < i1 ? sym_lc(i0 + k, (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu) : 0u;
+                nb += e[k] >> 24;
             }
-        });
-        if (nacc > 0) atomicOr(&words[wpos], (uint32_t)(acc >> 32));
+        }
+        uint32_t rbits = 0;
+        const uint32_t lb0 = (uint32_t)(bitpos & 31) + block_excl_scan<kEmitThreads>(nb, wsum, &rbits);
+        if (nb) {
+            uint64_t acc = 0;      // pending bits, left aligned at bit 63
+            uint32_t wpos = lb0 >> 5, nacc = lb0 & 31;
+            bool first_word = true;
+#pragma unroll
+            for (uint32_t k = 0; k < kEmitC; ++k) {
+                const uint32_t l = e[k] >> 24;
+                if (l) {
+                    acc |= ((uint64_t)(e[k] & 0xFFFFFFu) << (64 - l)) >> nacc;
+                    nacc += l;
+                    if (nacc >= 32) {
+                        const uint32_t wv = (uint32_t)(acc >> 32);
+                        if (first_word) atomicOr(&obuf[wpos], wv);
+                        else obuf[wpos] = wv;
+                        first_word = false;
+                        ++wpos;
+                        acc <<= 32;
+                        nacc -= 32;
+                    }
+                }
+            }
+            if (nacc > 0) atomicOr(&obuf[wpos], (uint32_t)(acc >> 32));
+        }
+        __syncthreads();
+        const uint32_t nfull = (uint32_t)(((bitpos & 31) + rbits) >> 5);
+        uint32_t* dst = words + (bitpos >> 5);
+        for (uint32_t i = t; i < nfull; i += kEmitThreads) dst[i] = obuf[i];
+        const uint32_t cv = obuf[nfull];
+        __syncthreads();
+        for (uint32_t i = 1 + t; i <= nfull; i += kEmitThreads) obuf[i] = 0;
+        if (t == 0) obuf[0] = cv;
+        __syncthreads();
+        bitpos += rbits;
     }
-    __syncthreads();
+    const uint64_t data_end = bitpos;
+    if (t == 0) {  // the last partial word, and zeros under the end marker
+        words[data_end >> 5] = (data_end & 31) ? obuf[0] : 0u;
+        for (uint64_t w = (data_end >> 5) + 1; w <= ((data_end + 80) >> 5) + 1; ++w) words[w] = 0;
+    }
     if (t == 0) {
         uint64_t p = data_end;
         auto put = [&](uint32_t nb2, uint32_t v) {
