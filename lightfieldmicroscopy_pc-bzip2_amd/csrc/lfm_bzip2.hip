@@ -288,11 +288,14 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t wlim = B.cap - 8;  // RLE1 bytes past this are not stored (the stream goes to the host)
     // this thread's 32 bytes of a tile; the next tile's are loaded while this
     // one is processed
+    // (unconditional loads at clamped offsets: a load under a branch makes the
+    // compiler wait for every outstanding load at the next use)
+    const uint32_t glim = FROM_IMG ? L - 16 : B.raw_cap - 16;  // L >= 16: rows are whole 16-byte pieces
     auto load_chunk = [&](uint32_t g, uint32_t nv, uint4& a, uint4& b) {
-        a = make_uint4(0, 0, 0, 0);
-        b = make_uint4(0, 0, 0, 0);
-        if (nv) a = load16(g);
-        if (nv > 16) b = load16(g + 16);
+        const uint4 va = load16(min(g, glim)), vb = load16(min(g + 16, glim));
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        a = nv ? va : z;
+        b = nv > 16 ? vb : z;
     };
     uint4 na, nb;
     {
@@ -518,18 +521,18 @@ struct BktPart {
 
 __device__ __forceinline__ BktPart bucket_fetch(const uint8_t* __restrict__ T, uint32_t n, uint32_t i0)
 {
-    BktPart p{0u, 0u};
-    if (i0 >= n) return p;
+    // loads at clamped offsets for every thread (no load under a branch: the
+    // compiler would wait for all outstanding loads at the next use)
     const uint32_t t = threadIdx.x;
-    const uint32_t m = min(n - i0, kBktTile);
-    if (4 * t < m) p.w = *(const uint32_t*)(T + i0 + 4 * t);  // may read up to 3 bytes past n: inside the stream's cap
-    if (t < 8) {
-        uint32_t j = i0 + m + t;
-        while (j >= n) j -= n;
-        p.e = T[j];
-    } else if (t == 8) {
-        p.e = T[i0 ? i0 - 1 : n - 1];
-    }
+    const uint32_t i0c = min(i0, n ? n - 1 : 0u);
+    const uint32_t m = n > i0c ? min(n - i0c, kBktTile) : 0u;
+    // 4 bytes (may read up to 3 bytes past n: inside the stream's cap)
+    const uint32_t w = *(const uint32_t*)(T + min(i0c + 4 * t, n ? (n - 1) & ~3u : 0u));
+    uint32_t j = n ? (t < 8 ? (i0c + m + t) % n : (i0c ? i0c - 1 : n - 1)) : 0u;
+    const uint32_t e = T[j];
+    BktPart p;
+    p.w = (i0 < n && 4 * t < m) ? w : 0u;
+    p.e = (i0 < n && t <= 8) ? e : 0u;
     return p;
 }
 
@@ -1159,8 +1162,10 @@ __global__ __launch_bounds__(256) void mtf_last(Batch B, uint32_t nseg_max, int3
     __builtin_amdgcn_wave_barrier();
     uint8_t* llbuf = (uint8_t*)B.mtfv + o;  // the mtfv area is free until rle2
     const uint32_t j1 = min(n, j0 + kSeg);
+    uint32_t vn = B.sa[o + min(j0 + lane, j1 - 1)];  // loaded an iteration ahead (clamped, unconditional)
     for (uint32_t j = j0 + lane; j < j1; j += 64) {
-        const uint32_t v = B.sa[o + j];
+        const uint32_t v = vn;
+        vn = B.sa[o + min(j + 64, j1 - 1)];
         if ((v & kIdxMask) == 0) B.orig_ptr[s] = j;  // BZ2_blockSort: origPtr = sorted position of rotation 0
         const uint32_t ll = u2s[wave][v >> 24];
         llbuf[j] = (uint8_t)ll;
@@ -1389,10 +1394,15 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
     uint8_t* mraw = B.uflag + o;
     const uint32_t je = min(n, js + kSeg);
     const uint64_t lt = (1ull << lane) - 1ull, gt = ~lt & ~(1ull << lane);
+    // the next window's symbol is loaded a window ahead, unconditionally (a
+    // clamped index): a load under a branch made the compiler wait for every
+    // outstanding load at the next use
+    uint32_t cn = llbuf[min(js + lane, je - 1)];
     for (uint32_t j0 = js; j0 < je; j0 += 64) {
         const uint32_t j = j0 + lane;
         const bool valid = j < je;
-        const uint32_t c = valid ? llbuf[j] : 0u;
+        const uint32_t c = valid ? cn : 0u;
+        cn = llbuf[min(j + 64, je - 1)];
         // match mask of c in this window
         if (valid) mt[wave][c] = 0;
         wsync();
@@ -1507,17 +1517,25 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         rtz = baz ? atz + btz : btz;
         raz = aaz & baz;
     };
+    // this thread's 64 values of a tile, in registers, loaded a tile ahead
+    uint4 nq[kRle2Per / 16];
+    auto load_vals = [&](uint32_t tb2) {
+        const uint32_t a0 = min(n, tb2 + t * kRle2Per), l2 = min(n, a0 + kRle2Per) - a0;
+#pragma unroll
+        for (uint32_t i = 0; i < kRle2Per / 16; ++i)
+            nq[i] = 16 * i < l2 ? *(const uint4*)(m + a0 + 16 * i) : make_uint4(0, 0, 0, 0);
+    };
+    load_vals(0);
     __syncthreads();
     for (uint32_t tb = 0; tb < n; tb += kRle2Tile) {
         const uint32_t c0 = min(n, tb + t * kRle2Per), c1 = min(n, c0 + kRle2Per), len = c1 - c0;
         const bool last_tile = tb + kRle2Tile >= n;
-        // this thread's values, once, in registers
         uint32_t q[kRle2Per / 4];
 #pragma unroll
         for (uint32_t i = 0; i < kRle2Per / 16; ++i) {
-            const uint4 v = 16 * i < len ? *(const uint4*)(m + c0 + 16 * i) : make_uint4(0, 0, 0, 0);
-            q[4 * i] = v.x; q[4 * i + 1] = v.y; q[4 * i + 2] = v.z; q[4 * i + 3] = v.w;
+            q[4 * i] = nq[i].x; q[4 * i + 1] = nq[i].y; q[4 * i + 2] = nq[i].z; q[4 * i + 3] = nq[i].w;
         }
+        load_vals(tb + kRle2Tile);
         auto each = [&](auto&& f) {
 #pragma unroll
             for (uint32_t i = 0; i < kRle2Per; ++i)
