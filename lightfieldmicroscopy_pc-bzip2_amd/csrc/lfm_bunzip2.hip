@@ -766,9 +766,35 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
         }
         return;
     }
-    // C: decode the segment from its start state
+    // C: decode the segment from its start state.  Whole aligned 16-byte
+    // pieces of the lane's output leave as one store each (byte stores made
+    // every store instruction touch 64 scattered lines); the partial pieces at
+    // the ends, shared with the neighbouring lanes, go byte by byte.
     {
         uint32_t s1 = sst[lane], o = soff[lane], prevb = before;
+        const uint32_t oend = lane < 63 ? soff[lane + 1] : tot;
+        // pieces are aligned in memory: po = o + (out's address mod 16)
+        const uint32_t ab = (uint32_t)((uintptr_t)out & 15u);
+        const uint32_t hbeg = min(((o + ab + 15) & ~15u) - ab, oend);
+        const uint32_t tbeg = max(((oend + ab) & ~15u) - ab, hbeg);
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;  // the piece holding o
+        auto put = [&](uint32_t c) {
+            if (o < hbeg || o >= tbeg) {
+                out[o] = (uint8_t)c;
+            } else {
+                const uint32_t po = o + ab;
+                const uint32_t k = (po >> 2) & 3u, v = c << (8 * (po & 3u));
+                a0 |= k == 0 ? v : 0u;
+                a1 |= k == 1 ? v : 0u;
+                a2 |= k == 2 ? v : 0u;
+                a3 |= k == 3 ? v : 0u;
+                if ((po & 15u) == 15u) {
+                    *(uint4*)(out + (o - 15)) = make_uint4(a0, a1, a2, a3);
+                    a0 = a1 = a2 = a3 = 0;
+                }
+            }
+            ++o;
+        };
         uint4 q = tx.load(a), nq = tx.load(a + 16);
         for (uint32_t i = a; i < b; i += 16) {
 #pragma unroll
@@ -776,11 +802,10 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
                 if (i + j < b) {
                     const uint32_t c = chunk_byte(q, j);
                     if (s1 == 4) {  // count byte: c more copies of the previous byte
-                        for (uint32_t k = 0; k < c; ++k) out[o + k] = (uint8_t)prevb;
-                        o += c;
+                        for (uint32_t k = 0; k < c; ++k) put(prevb);
                         s1 = 0;
                     } else {
-                        out[o++] = (uint8_t)c;
+                        put(c);
                         s1 = (s1 == 0 || c != prevb) ? 1u : s1 + 1u;
                     }
                     prevb = c;
