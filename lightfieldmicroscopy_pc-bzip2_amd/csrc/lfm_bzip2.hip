@@ -1162,18 +1162,40 @@ __global__ __launch_bounds__(256) void mtf_last(Batch B, uint32_t nseg_max, int3
     __builtin_amdgcn_wave_barrier();
     uint8_t* llbuf = (uint8_t*)B.mtfv + o;  // the mtfv area is free until rle2
     const uint32_t j1 = min(n, j0 + kSeg);
-    uint32_t vn = B.sa[o + min(j0 + lane, j1 - 1)];  // loaded an iteration ahead (clamped, unconditional)
-    for (uint32_t j = j0 + lane; j < j1; j += 64) {
-        const uint32_t v = vn;
-        vn = B.sa[o + min(j + 64, j1 - 1)];
-        if ((v & kIdxMask) == 0) B.orig_ptr[s] = j;  // BZ2_blockSort: origPtr = sorted position of rotation 0
-        const uint32_t ll = u2s[wave][v >> 24];
-        llbuf[j] = (uint8_t)ll;
-        // only the last position of each run of equal symbols (the next lane
-        // holds position j + 1) can be the symbol's last: the BWT output is
-        // runs, and 64 lanes on one LDS word serialise
-        const uint32_t nxt = (uint32_t)__builtin_amdgcn_mov_dpp((int)ll, 0x130, 0xF, 0xF, false);  // wave_shl:1
-        if (lane == 63 || j + 1 >= j1 || nxt != ll) atomicMax(&last[wave][ll], (int32_t)j);
+    // four consecutive positions per lane (16-byte loads of sa, 4-byte stores
+    // of the symbols), loaded an iteration ahead at a clamped, aligned index
+    // (sa holds cap >= n + 8 entries per stream)
+    const uint32_t jlast = (j1 - 1) & ~3u;
+    uint4 vn = *(const uint4*)(B.sa + o + min(j0 + 4 * lane, jlast));
+    for (uint32_t jb = j0; jb < j1; jb += 256) {
+        const uint32_t j = jb + 4 * lane;
+        const uint4 v4 = vn;
+        vn = *(const uint4*)(B.sa + o + min(j + 256, jlast));
+        const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
+        uint32_t ll[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            ll[q] = u2s[wave][v[q] >> 24];
+            if (j + q < j1 && (v[q] & kIdxMask) == 0) B.orig_ptr[s] = j + q;  // BZ2_blockSort: origPtr = sorted position of rotation 0
+        }
+        if (j + 3 < j1) {
+            *(uint32_t*)(llbuf + j) = ll[0] | (ll[1] << 8) | (ll[2] << 16) | (ll[3] << 24);
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q)
+                if (j + q < j1) llbuf[j + q] = (uint8_t)ll[q];
+        }
+        // only the last position of each run of equal symbols can be the
+        // symbol's last: the BWT output is runs, and 64 lanes on one LDS word
+        // serialise
+        const uint32_t nxt0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)ll[0], 0x130, 0xF, 0xF, false);  // wave_shl:1
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t pos = j + q;
+            const uint32_t nx = q < 3 ? ll[q + 1] : nxt0;
+            const bool end = pos + 1 >= j1 || (q == 3 && lane == 63) || nx != ll[q];
+            if (pos < j1 && end) atomicMax(&last[wave][ll[q]], (int32_t)pos);
+        }
     }
     __builtin_amdgcn_wave_barrier();
     int32_t* dst = seg_last + ((size_t)s * nseg_max + k) * 256;
