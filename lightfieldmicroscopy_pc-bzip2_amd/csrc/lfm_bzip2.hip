@@ -1443,12 +1443,24 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
         } else {
             m = P0;
         }
-        // first occurrences: earlier first-occurrence symbols placed behind c
-        const uint64_t F = ballot64(valid && !has_prev);
-        for (uint64_t f = F & ~(1ull << 63); f; f &= f - 1ull) {
-            const uint32_t i = (uint32_t)__builtin_ctzll(f);
-            const uint32_t pi = __builtin_amdgcn_readlane(P0, i);
-            m += (!has_prev && lane > i && pi > P0) ? 1u : 0u;
+        // first occurrences: earlier first-occurrence symbols placed behind c.
+        // Their ranks at the window start are distinct, so the count is the
+        // number of bits above P0 in the exclusive prefix OR of the earlier
+        // first-occurrence lanes' one-hot ranks (8 words, DPP scans); a
+        // serial loop over them (~27 per window, a readlane each) was
+        // scalar-unit bound
+        {
+            const bool isF = valid && !has_prev;
+            const uint32_t pw = P0 >> 5, pb = P0 & 31u;
+            uint32_t cnt = 0;
+#pragma unroll
+            for (uint32_t wd = 0; wd < 8; ++wd) {
+                const uint32_t oh = (isF && pw == wd) ? (1u << pb) : 0u;
+                const uint32_t pre = wave_or_scan_excl32(oh);
+                const uint32_t above = wd > pw ? ~0u : (wd == pw ? (pb == 31 ? 0u : ~0u << (pb + 1)) : 0u);
+                cnt += (uint32_t)__popc(pre & above);
+            }
+            if (isF) m += cnt;
         }
         if (valid) mraw[j] = (uint8_t)m;
         // list update: window symbols by last occurrence, then the rest
