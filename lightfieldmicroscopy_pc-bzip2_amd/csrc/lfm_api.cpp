@@ -1,4 +1,7 @@
 // lfm_api.cpp -- liblfm extensions (lfm_api.h).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include "lfm_api.h"
 #include <cstdlib>
 #include <cstring>
@@ -211,9 +214,14 @@ extern "C" int lfm_place_slab(const uint8_t* slab, uint64_t slab_len, uint8_t* d
 
 extern "C" int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads)
 {
+    const auto t0 = std::chrono::steady_clock::now();
     klb_image_header h;
     int rc = h.parseHeader(buf, len);
     if (rc) return rc;
     const size_t hs = h.getSizeInBytes();
-    return lfm::decode_payload(buf + hs, len - hs, h, (uint8_t*)img, numThreads, lfm::current_family());
+    rc = lfm::decode_payload(buf + hs, len - hs, h, (uint8_t*)img, numThreads, lfm::current_family());
+    if (std::getenv("LFM_DECODE_TIMING"))
+        std::fprintf(stderr, "decode total (C)     %8.2f ms\n",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return rc;
 }

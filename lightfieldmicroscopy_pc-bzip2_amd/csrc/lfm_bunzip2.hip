@@ -460,22 +460,23 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
 // ------------------------------------------------------------ inverse BWT --
 constexpr int kTtThreads = 256;
 
-__global__ __launch_bounds__(kTtThreads) void bzd_tt(Dec D)
+template <int NT>
+__global__ __launch_bounds__(NT) void bzd_tt(Dec D)
 {
     __shared__ uint32_t cf[256];       // C[c]: bytes < c
     __shared__ uint32_t run[256];      // occurrences of c before the current tile
-    __shared__ uint32_t wc[kTtThreads / 64][256];
+    __shared__ uint32_t wc[NT / 64][256];
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (D.flags[s]) return;
     const uint32_t n = D.n[s];
     const uint8_t* ll = D.ll + (size_t)s * D.cap;
     uint32_t* tt = D.tt + (size_t)s * D.cap;
-    for (uint32_t c = t; c < 256; c += kTtThreads) {
+    for (uint32_t c = t; c < 256; c += NT) {
         run[c] = 0;
-        for (int w = 0; w < kTtThreads / 64; ++w) wc[w][c] = 0;
+        for (int w = 0; w < NT / 64; ++w) wc[w][c] = 0;
     }
     __syncthreads();
-    for (uint32_t i = t; i < n; i += kTtThreads) atomicAdd(&run[ll[i]], 1u);
+    for (uint32_t i = t; i < n; i += NT) atomicAdd(&run[ll[i]], 1u);
     __syncthreads();
     if (t < 64) {  // exclusive scan of the 256 counts, 4 per lane
         uint32_t v[4], sum = 0;
@@ -495,11 +496,11 @@ __global__ __launch_bounds__(kTtThreads) void bzd_tt(Dec D)
         }
     }
     __syncthreads();
-    for (uint32_t c = t; c < 256; c += kTtThreads) run[c] = 0;
+    for (uint32_t c = t; c < 256; c += NT) run[c] = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
-    // LF(i) = C[c] + Occ(c, i) in tiles of kTtThreads positions
-    for (uint32_t i0 = 0; i0 < n; i0 += kTtThreads) {
+    // LF(i) = C[c] + Occ(c, i) in tiles of NT positions
+    for (uint32_t i0 = 0; i0 < n; i0 += NT) {
         const uint32_t i = i0 + t;
         const bool ok = i < n;
         const uint32_t c = ok ? ll[i] : 256u;
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(kTtThreads) void bzd_tt(Dec D)
         __syncthreads();
         uint32_t before = 0, total = 0;
         if (ok) {
-            for (uint32_t w = 0; w < kTtThreads / 64; ++w) {
+            for (uint32_t w = 0; w < NT / 64; ++w) {
                 const uint32_t x = wc[w][c];
                 before += w < wave ? x : 0u;
                 total += x;
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(kTtThreads) void bzd_tt(Dec D)
     }
     __syncthreads();
     // decompress.c's fast tt: tt[j] = next << 8 | ll[j]
-    for (uint32_t j = t; j < n; j += kTtThreads) tt[j] = (tt[j] << 8) | ll[j];
+    for (uint32_t j = t; j < n; j += NT) tt[j] = (tt[j] << 8) | ll[j];
 }
 
 // marker id of node j (or ~0u): every kMark-th node, and the walk's start
@@ -541,27 +542,32 @@ __device__ __forceinline__ uint32_t marker_id(uint32_t j, uint32_t v0, uint32_t 
     return j == v0 ? nm : ~0u;
 }
 
-__global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
+// LDSM: the marker tables (successor, length, output offset, restart node)
+// live in LDS, so the one-lane chaining of the segments reads LDS instead of
+// making ~1 150 dependent global round trips per stream
+template <int NT, bool LDSM>
+__global__ __launch_bounds__(NT) void bzd_walk(Dec D)
 {
+    extern __shared__ uint32_t wsm[];  // LDSM: 4 x mcap words
     __shared__ uint32_t s_total;
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     if (D.flags[s]) return;
     const uint32_t n = D.n[s];
     const uint32_t* tt = D.tt + (size_t)s * D.cap;
     uint8_t* rle = D.rle + (size_t)s * D.cap;
-    uint32_t* mnext = D.mnext + (size_t)s * D.mcap;
-    uint32_t* mlen = D.mlen + (size_t)s * D.mcap;
-    uint32_t* mstart = D.mstart + (size_t)s * D.mcap;
+    uint32_t* mnext = LDSM ? wsm : D.mnext + (size_t)s * D.mcap;
+    uint32_t* mlen = LDSM ? wsm + D.mcap : D.mlen + (size_t)s * D.mcap;
+    uint32_t* mstart = LDSM ? wsm + 2 * D.mcap : D.mstart + (size_t)s * D.mcap;
+    uint32_t* mres = LDSM ? wsm + 3 * D.mcap : D.mres + (size_t)s * D.mcap;
     const uint32_t v0 = tt[D.orig[s]] >> 8;
     const uint32_t nm = (n + kMark - 1) / kMark;  // regular markers 0 .. nm-1, the start is nm
     const bool extra = (v0 % kMark) != 0;
     const uint32_t nwalk = nm + (extra ? 1u : 0u);
     auto node_of = [&](uint32_t id) { return id < nm ? id * kMark : v0; };
-    uint32_t* mres = D.mres + (size_t)s * D.mcap;
     uint8_t* keep = D.wkeep + (size_t)s * D.mcap * kWalkKeep;
     // pass 1: segment lengths and successors; the walker keeps the bytes it
     // passes (the low byte of each tt entry it reads) in dwords
-    for (uint32_t id = t; id < nwalk; id += kTtThreads) {
+    for (uint32_t id = t; id < nwalk; id += NT) {
         uint32_t pos = node_of(id), len = 0, nx = ~0u, acc = 0, res = 0;
         uint32_t* kp = (uint32_t*)(keep + (size_t)id * kWalkKeep);
         do {
@@ -602,13 +608,13 @@ __global__ __launch_bounds__(kTtThreads) void bzd_walk(Dec D)
     }
     // pass 2: the kept bytes into place, one wave per segment
     const uint32_t lane = t & 63, wave = t >> 6;
-    for (uint32_t id = wave; id < nwalk; id += kTtThreads / 64) {
+    for (uint32_t id = wave; id < nwalk; id += NT / 64) {
         const uint32_t o = mstart[id], m = min(mlen[id], kWalkKeep);
         const uint8_t* src = keep + (size_t)id * kWalkKeep;
         for (uint32_t k = lane; k < m; k += 64) rle[o + k] = src[k];
     }
     // segments longer than kWalkKeep: walk on from where their walker stopped keeping
-    for (uint32_t id = t; id < nwalk; id += kTtThreads) {
+    for (uint32_t id = t; id < nwalk; id += NT) {
         const uint32_t len = mlen[id];
         if (len <= kWalkKeep) continue;
         uint32_t pos = mres[id], o = mstart[id] + kWalkKeep;
@@ -957,8 +963,38 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     if (lut_bits == 10) hipLaunchKernelGGL(bzd_huff<10>, dim3(count), dim3(64), sel_lds, st, D);
     else if (lut_bits == 9) hipLaunchKernelGGL(bzd_huff<9>, dim3(count), dim3(64), sel_lds, st, D);
     else hipLaunchKernelGGL(bzd_huff<8>, dim3(count), dim3(64), sel_lds, st, D);
-    hipLaunchKernelGGL(bzd_tt, dim3(count), dim3(kTtThreads), 0, st, D);
-    hipLaunchKernelGGL(bzd_walk, dim3(count), dim3(kTtThreads), 0, st, D);
+    // LF mapping: LFM_TT_THREADS (256 / 512 / 1024 positions per tile) for A/B runs
+    static const int tt_nt = [] {
+        const char* e = getenv("LFM_TT_THREADS");
+        const int v = e ? atoi(e) : kTtThreads;
+        return v == 512 || v == 1024 ? v : 256;
+    }();
+    if (tt_nt == 1024) hipLaunchKernelGGL(bzd_tt<1024>, dim3(count), dim3(1024), 0, st, D);
+    else if (tt_nt == 512) hipLaunchKernelGGL(bzd_tt<512>, dim3(count), dim3(512), 0, st, D);
+    else hipLaunchKernelGGL(bzd_tt<256>, dim3(count), dim3(256), 0, st, D);
+    // inverse-BWT walk: LFM_WALK_THREADS (256 / 512 (default) / 1024 per stream) and
+    // LFM_WALK_LDSM (marker tables in LDS, default on) for A/B runs
+    static const int walk_nt = [] {
+        const char* e = getenv("LFM_WALK_THREADS");
+        const int v = e ? atoi(e) : 512;
+        return v == 256 || v == 1024 ? v : 512;
+    }();
+    static const bool walk_ldsm = [] {
+        const char* e = getenv("LFM_WALK_LDSM");
+        return e ? atoi(e) != 0 : true;
+    }();
+    // (large blocks, level 5 and up, keep the tables in global memory: LDS
+    // for ~2 workgroups per CU at most)
+    const size_t wl = (size_t)D.mcap * 16;
+    if (walk_ldsm && wl <= 48 * 1024) {
+        if (walk_nt == 1024) hipLaunchKernelGGL((bzd_walk<1024, true>), dim3(count), dim3(1024), wl, st, D);
+        else if (walk_nt == 512) hipLaunchKernelGGL((bzd_walk<512, true>), dim3(count), dim3(512), wl, st, D);
+        else hipLaunchKernelGGL((bzd_walk<256, true>), dim3(count), dim3(256), wl, st, D);
+    } else {
+        if (walk_nt == 1024) hipLaunchKernelGGL((bzd_walk<1024, false>), dim3(count), dim3(1024), 0, st, D);
+        else if (walk_nt == 512) hipLaunchKernelGGL((bzd_walk<512, false>), dim3(count), dim3(512), 0, st, D);
+        else hipLaunchKernelGGL((bzd_walk<256, false>), dim3(count), dim3(256), 0, st, D);
+    }
     hipLaunchKernelGGL(bzd_rle1, dim3(count), dim3(64), 0, st, D);
     if (hipGetLastError() != hipSuccess) return LFM_HIP_ERUNTIME;
     if (hipMemcpyAsync(h_lens, D.out_len, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -1491,7 +1491,13 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     }
     phase("alloc");
     int rc = 0;
-    if (!staged_h2d(d_pay, payload, offs[nb], st, threads) ||
+    // the payload goes up with one runtime copy: the pinned-chunk staging
+    // (staged_h2d) ran its chunks through blit kernels at ~8 GB/s (35 ms for
+    // config 3's 277 MB) where the runtime's own pageable path reaches
+    // ~55 GB/s; LFM_DECODE_STAGED_H2D=1 keeps the staging for A/B runs
+    static const bool staged_up = env_int("LFM_DECODE_STAGED_H2D", 0) != 0;
+    if (!(staged_up ? staged_h2d(d_pay, payload, offs[nb], st, threads)
+                    : hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) == hipSuccess) ||
         hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, st) != hipSuccess)
         rc = 3;
     phase("upload");

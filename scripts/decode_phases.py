@@ -24,6 +24,7 @@ buf, _ = enc.encode_slab(d, 0, header_version=forced_request(k), nnum=T, copy=Fa
 buf = bytes(buf)
 ref = d.cpu().numpy().view(np.uint16)
 for it in range(3):
+    img = None  # free the previous result first (its unmap is not the decode's)
     t0 = time.perf_counter()
     img = lfm.decode(buf)
     ms = (time.perf_counter() - t0) * 1e3
