@@ -219,7 +219,8 @@ int MemSink::finish(const klb_image_header& h)
 // leave the CUs and their caches to the compute.  Returns false (the caller
 // falls back to hipMemcpyAsync) if HSA cannot take the copy; LFM_D2H_SDMA=0
 // disables it.  The caller has synchronised the producing stream.
-static bool sdma_d2h(void* dst, const void* src, size_t n)
+// the HSA CPU agent (SDMA copies are enabled and HSA is up), or null
+static const hsa_agent_t* hsa_cpu_agent()
 {
     struct Cpu {
         bool ok = false;
@@ -243,7 +244,13 @@ static bool sdma_d2h(void* dst, const void* src, size_t n)
         }
     };
     static Cpu cpu;
-    if (!cpu.ok || n == 0) return cpu.ok;
+    return cpu.ok ? &cpu.agent : nullptr;
+}
+
+static bool sdma_d2h(void* dst, const void* src, size_t n)
+{
+    const hsa_agent_t* cpu = hsa_cpu_agent();
+    if (!cpu || n == 0) return cpu != nullptr;
     hsa_amd_pointer_info_t info;
     std::memset(&info, 0, sizeof(info));
     info.size = sizeof(info);
@@ -252,7 +259,7 @@ static bool sdma_d2h(void* dst, const void* src, size_t n)
         return false;
     hsa_signal_t sig;
     if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return false;
-    bool ok = hsa_amd_memory_async_copy(dst, cpu.agent, src, info.agentOwner, n, 0, nullptr, sig) == HSA_STATUS_SUCCESS;
+    bool ok = hsa_amd_memory_async_copy(dst, *cpu, src, info.agentOwner, n, 0, nullptr, sig) == HSA_STATUS_SUCCESS;
     if (ok)
         ok = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) == 0;
     hsa_signal_destroy(sig);
@@ -1342,6 +1349,62 @@ bool staged_h2d(void* d_dst, const void* h_src, size_t n, hipStream_t st, int th
     return true;
 }
 
+// Host -> device through the pinned chunks with the DMA on an SDMA engine
+// (HSA): the host copy of one chunk overlaps the engine's copy of the other.
+// The blit-kernel copies of hipMemcpyAsync ran the decode payload upload at
+// 5-47 ms depending on the process's state; the engine does not depend on
+// the CUs.  Returns false if HSA cannot take the copy (nothing was issued on
+// a false return before the first chunk; the caller falls back).  The
+// destination stream must be idle (the caller synchronises it).
+bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
+{
+    const hsa_agent_t* cpu = hsa_cpu_agent();
+    Staging& S = staging();
+    if (!cpu || !S.ready() || n == 0) return false;
+    hsa_amd_pointer_info_t info;
+    std::memset(&info, 0, sizeof(info));
+    info.size = sizeof(info);
+    if (hsa_amd_pointer_info(d_dst, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        info.type != HSA_EXT_POINTER_TYPE_HSA)
+        return false;
+    hsa_signal_t sig[2];
+    if (hsa_signal_create(0, 0, nullptr, &sig[0]) != HSA_STATUS_SUCCESS) return false;
+    if (hsa_signal_create(0, 0, nullptr, &sig[1]) != HSA_STATUS_SUCCESS) {
+        hsa_signal_destroy(sig[0]);
+        return false;
+    }
+    bool ok = true;
+    static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
+    double t_wait = 0, t_copy = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    for (size_t off = 0, i = 0; ok && off < n; off += Staging::kChunk, ++i) {
+        const int b = (int)(i & 1);
+        const size_t len = std::min(Staging::kChunk, n - off);
+        auto t0 = now();
+        if (i >= 2) ok = hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                                   HSA_WAIT_STATE_BLOCKED) == 0;
+        if (!ok) break;
+        auto t1 = now();
+        par_memcpy_impl(S.buf[b], (const uint8_t*)h_src + off, len, threads);
+        t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        t_copy += std::chrono::duration<double, std::milli>(now() - t1).count();
+        hsa_signal_store_relaxed(sig[b], 1);
+        ok = hsa_amd_memory_async_copy((uint8_t*)d_dst + off, info.agentOwner, S.buf[b], *cpu, len, 0, nullptr,
+                                       sig[b]) == HSA_STATUS_SUCCESS;
+        if (!ok) hsa_signal_store_relaxed(sig[b], 0);
+    }
+    for (int b = 0; b < 2; ++b)
+        if (hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) != 0)
+            ok = false;
+    if (timing)
+        std::fprintf(stderr, "sdma h2d: %zu bytes, host copies %.2f ms, waits %.2f ms, %d threads\n", n, t_copy, t_wait,
+                     threads);
+    hsa_signal_destroy(sig[0]);
+    hsa_signal_destroy(sig[1]);
+    S.used[0] = S.used[1] = false;  // the chunks are free (no HIP event pending on them)
+    return ok;
+}
+
 bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads)
 {
     Staging& S = staging();
@@ -1491,13 +1554,22 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     }
     phase("alloc");
     int rc = 0;
-    // the payload goes up with one runtime copy: the pinned-chunk staging
-    // (staged_h2d) ran its chunks through blit kernels at ~8 GB/s (35 ms for
-    // config 3's 277 MB) where the runtime's own pageable path reaches
-    // ~55 GB/s; LFM_DECODE_STAGED_H2D=1 keeps the staging for A/B runs
-    static const bool staged_up = env_int("LFM_DECODE_STAGED_H2D", 0) != 0;
-    if (!(staged_up ? staged_h2d(d_pay, payload, offs[nb], st, threads)
-                    : hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) == hipSuccess) ||
+    // the payload upload: blit-kernel copies (the runtime's pageable path or
+    // hipMemcpyAsync from the pinned chunks) took 5-47 ms for config 3's
+    // 277 MB depending on the process's state; an SDMA engine does not
+    // LFM_DECODE_H2D: 0 SDMA engine through the pinned chunks (default;
+    // falls back to 1 when HSA cannot take it), 1 one runtime copy, 2 the
+    // pinned chunks with hipMemcpyAsync
+    static const int up_mode = env_int("LFM_DECODE_H2D", 0);
+    bool up_ok = false;
+    if (up_mode == 0) {
+        up_ok = hipStreamSynchronize(st) == hipSuccess && sdma_staged_h2d(d_pay, payload, offs[nb], threads);
+        if (!up_ok) (void)hipGetLastError();
+    }
+    if (!up_ok)
+        up_ok = up_mode == 2 ? staged_h2d(d_pay, payload, offs[nb], st, threads)
+                             : hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) == hipSuccess;
+    if (!up_ok ||
         hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, st) != hipSuccess)
         rc = 3;
     phase("upload");
