@@ -76,6 +76,7 @@ struct Dec {
     uint32_t* flags;
     uint32_t* out_len;
     uint32_t sel_cap;         // selectors that fit the decoder's LDS
+    uint32_t dpp_scan;        // 1: output offsets by a DPP wave scan (LFM_BZD_DPP, default), 0: shuffles
 };
 
 // MSB-first bit reader over the payload: a 64-bit window of two big-endian
@@ -204,6 +205,24 @@ struct WaveBits {
     __device__ __forceinline__ bool over() const { return 32 * (wi - 2) + off > total; }
 };
 
+// inclusive wave sum by DPP row shifts and row broadcasts (no LDS round
+// trips; the lanes a step has no source for add 0)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_in(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_sum_incl(uint32_t x)
+{
+    x += dpp_in<0x111, 0xF>(x);  // row_shr:1
+    x += dpp_in<0x112, 0xF>(x);  // row_shr:2
+    x += dpp_in<0x114, 0xF>(x);  // row_shr:4
+    x += dpp_in<0x118, 0xF>(x);  // row_shr:8
+    x += dpp_in<0x142, 0xA>(x);  // row_bcast:15 into rows 1 and 3
+    x += dpp_in<0x143, 0xC>(x);  // row_bcast:31 into rows 2 and 3
+    return x;
+}
+
 template <int LB>
 __global__ __launch_bounds__(64) void bzd_huff(Dec D)
 {
@@ -219,6 +238,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
     extern __shared__ uint32_t sel[];
     const uint32_t lane = threadIdx.x;
     const uint32_t s = blockIdx.x;
+    const bool dpp_scan = D.dpp_scan != 0;
     uint32_t flag = 0;
     WaveBits br;
     const uint64_t b0 = D.offs[s], b1 = D.offs[s + 1];
@@ -421,10 +441,15 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             const uint32_t fb = (uint32_t)__shfl((int)outb, max(p, 0));
             const uint32_t b = isrun ? (p < 0 ? front0 : fb) : outb;
             // 3. offsets (exclusive prefix sum of the counts) and the stores
-            uint32_t incl = cnt;
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-                if ((int)lane >= d) incl += o;
+            uint32_t incl;
+            if (dpp_scan) {
+                incl = wave_sum_incl(cnt);
+            } else {
+                incl = cnt;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+                    if ((int)lane >= d) incl += o;
+                }
             }
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             if (nblock + total > cap) { flag = kHost; break; }
@@ -954,6 +979,11 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     if (hipMemcpyAsync(d_offs, h_offs, ((size_t)count + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
     D.sel_cap = std::min<uint32_t>(kMaxSel, (D.cap + 49) / 50 + 64);
+    static const uint32_t dpp_env = [] {
+        const char* e = getenv("LFM_BZD_DPP");
+        return e ? (uint32_t)(atoi(e) != 0) : 1u;
+    }();
+    D.dpp_scan = dpp_env;
     const size_t sel_lds = ((D.sel_cap + 7) / 8 * 4 + 15) & ~(size_t)15;
     static const int lut_bits = [] {
         const char* e = getenv("LFM_BZD_LUT_BITS");

@@ -593,3 +593,31 @@ def test_pipelined_submit_wait(lfmlib, oracle, gpu):
         enc.close()
     finally:
         lfmlib.set_family("tiles")
+
+
+@pytest.mark.parametrize("env", ["LFM_DECODE_H2D=1", "LFM_DECODE_H2D=2",
+                                 "LFM_WALK_LDSM=0 LFM_WALK_THREADS=256", "LFM_WALK_THREADS=1024 LFM_TT_THREADS=1024"])
+def test_decode_path_switches(lfmlib, oracle, gpu, tmp_path, env):
+    """The decode's alternative paths (payload upload by one runtime copy or
+    by hipMemcpyAsync from the pinned chunks instead of the SDMA engine; walk
+    marker tables in global memory, other walk / LF-mapping widths) restore
+    the same pixels.  The switches are read once per process: each variant
+    decodes in its own child process (one GPU process at a time)."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    img = oracle.synthetic_lf(256, 192, Z=16, T=13, seed=5)
+    lfmlib.set_family("angle")
+    try:
+        p = tmp_path / "sw.lfm"
+        lfmlib.write_lfm(str(p), img, predictor_request=0, nnum=13, video=0)
+    finally:
+        lfmlib.set_family("tiles")
+    out = tmp_path / "out.npy"
+    code = ("import sys; sys.path.insert(0, %r); import numpy as np, lfm; lfm.set_family('angle'); "
+            "o, _, _ = lfm.read_lfm(%r); np.save(%r, o)" % (PKG, str(p), str(out)))
+    child_env = dict(os.environ)
+    child_env.update(kv.split("=", 1) for kv in env.split())
+    r = subprocess.run([sys.executable, "-c", code], env=child_env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert np.array_equal(np.load(out).reshape(img.shape), img), env
