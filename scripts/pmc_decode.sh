@@ -1,6 +1,6 @@
 #!/bin/bash
 # Instruction-mix counters of the decode kernels (one PMC pass per set).
-# usage: scripts/pmc_decode.sh OUTDIR
+# usage: scripts/pmc_decode.sh OUTDIR   (one config-3 encode + three decodes per pass)
 set -u
 OUT=$1
 mkdir -p "$OUT"
@@ -9,7 +9,7 @@ i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" ; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$OUT/p$i" -o pmc -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/p$i.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$OUT/p$i" -o pmc -- python scripts/decode_phases.py > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/p$i.log"; exit $rc; fi
