@@ -621,3 +621,70 @@ def test_decode_path_switches(lfmlib, oracle, gpu, tmp_path, env):
     r = subprocess.run([sys.executable, "-c", code], env=child_env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     assert np.array_equal(np.load(out).reshape(img.shape), img), env
+
+
+def test_decode_threads_release_device_memory(lfmlib, oracle, gpu, tmp_path):
+    """Decodes from short-lived host threads free their per-thread device
+    buffers and pinned staging when the thread exits: the
+    device's free memory does not shrink with the number of threads."""
+    import threading
+    torch = gpu
+    img = oracle.synthetic_lf(1024, 1024, Z=16, T=13, seed=9)
+    p = tmp_path / "thr.lfm"
+    lfmlib.write_lfm(str(p), img, predictor_request=8 + 4, nnum=13)
+    buf = p.read_bytes()
+    errors = []
+
+    def one():
+        try:
+            if not np.array_equal(lfmlib.decode(buf).reshape(img.shape), img):
+                errors.append("pixels")
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    def run_thread():
+        th = threading.Thread(target=one)
+        th.start()
+        th.join()
+
+    run_thread()
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    for _ in range(6):
+        run_thread()
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert not errors, errors
+    assert free0 - free1 < (128 << 20), (free0, free1)
+
+
+def test_encoder_rejects_bad_device_operands(lfmlib, gpu):
+    """Encoder._operand: strided views and unsupported dtypes
+    are refused instead of encoding the wrong pixels."""
+    torch = gpu
+    enc = lfmlib.Encoder(device=torch.cuda.current_device())
+    try:
+        d = torch.zeros((8, 64, 128), dtype=torch.int16, device="cuda")
+        with pytest.raises(lfmlib.LfmError):
+            enc.encode(d[:, :, ::2], nnum=13)
+        with pytest.raises(lfmlib.LfmError):
+            enc.encode(torch.zeros((8, 64, 64), dtype=torch.float16, device="cuda"), nnum=13)
+    finally:
+        enc.close()
+
+
+@pytest.mark.parametrize("fam", ["angle", "space"])
+def test_video_with_lossy_family_reads_loudly(lfmlib, oracle, gpu, tmp_path, fam):
+    """Video stacks with the angle / space families: the writer reproduces the
+    reference's bytes (with a warning: its temporal residual drops a bit) and
+    the reader refuses the file with an error instead of returning wrong
+    pixels."""
+    img = oracle.synthetic_lf(96, 96, Z=4, T=13, seed=3)
+    lfmlib.set_family(fam)
+    try:
+        p = tmp_path / "v.lfm"
+        lfmlib.write_lfm(str(p), img, predictor_request=8 + 4, nnum=13, video=1)
+        with pytest.raises(lfmlib.LfmError):
+            lfmlib.read_lfm(str(p))
+    finally:
+        lfmlib.set_family("tiles")
