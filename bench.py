@@ -369,8 +369,14 @@ def main():
     if world > 1:
         dist.barrier()
         shm.close()
-    if rank == 0 and world == 1 and not args.no_decode:
-        buf = bytes(b)
+    buf = bytes(b) if rank == 0 and world == 1 and not args.no_decode else None  # before b's buffer is reused
+    if rank == 0 and world == 1 and not args.no_host_input:
+        line["host_input"] = host_input_rates(enc, d_img, zf)
+    if buf is not None:
+        # the decode is a reader's job: it runs after the encoder (its buffers,
+        # pinned output and finisher threads) is released, as in a separate
+        # reader process
+        enc.close()
         ref = d_img.cpu().numpy().view(np.uint16)
         # three decodes, each into a fresh array (its first-touch page faults
         # timed): the first also pays one-time costs (lazily loaded kernels,
@@ -387,8 +393,6 @@ def main():
                           "first_ms": round(dlist[0], 1), "runs_ms": [round(x, 1) for x in dlist],
                           "exact": exact,
                           "path": "GPU bzip2 decode + GPU inverse predictor (host libbz2 only for flagged streams, %d threads)" % threads}
-    if rank == 0 and world == 1 and not args.no_host_input:
-        line["host_input"] = host_input_rates(enc, d_img, zf)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)
         line["cpu_baseline"]["affinity_cpus"] = len(os.sched_getaffinity(0))
