@@ -396,6 +396,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)
         line["cpu_baseline"]["affinity_cpus"] = len(os.sched_getaffinity(0))
+        line["cpu_baseline"]["threads_note"] = (
+            "cores = the threads used: this process's CPU share, min(affinity, OMP_NUM_THREADS=%s); "
+            "the box's affinity mask shows every host CPU, the job's share is OMP_NUM_THREADS"
+            % os.environ.get("OMP_NUM_THREADS", "unset"))
     if rank == 0:
         print(json.dumps(line), flush=True)
     enc.close()
