@@ -11,9 +11,9 @@ between steps.  After the timed steps (N=1) the last .lfm is decoded once
 in the JSON line, for information (not the metric).
 
 Multi-GPU (torchrun, one process per GPU): rank r encodes z-slab r (frames
-64r .. 64r+63) of a (world x 64)-frame stack; the predictor is selected on
-the stack's frame 0 redundantly on every rank (no broadcast) and forced for
-the slab.  Inside the timed region the ranks then build ONE .lfm of the whole
+64r .. 64r+63) of a (world x 64)-frame stack; every rank's submit selects the
+predictor on the stack's frame 0 (handed in as select_frame, redundantly on
+every rank: no broadcast) on the encoder's stream.  Inside the timed region the ranks then build ONE .lfm of the whole
 stack in host shared memory: an all_gather of every slab's (payload bytes,
 block count) -- the path's only exchange, RCCL under nccl -- gives each rank
 its payload offset and first block index, and every rank places its own
@@ -49,7 +49,7 @@ import torch  # noqa: E402  (before liblfm: one HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
 import lfm  # noqa: E402
-from lfm.shard import forced_request, max_over_ranks  # noqa: E402
+from lfm.shard import max_over_ranks  # noqa: E402
 
 X, Y, Z, T = 2048, 2048, 64, 15
 FAMILY = "angle"
@@ -247,10 +247,10 @@ def main():
     z0 = rank * zf
     lfm.synth_device(d_img, X, Y, zf, T, z0=z0, seed=SEED)
     if rank == 0:
-        d_f0 = d_img[0]
+        sel_frame = None  # frame 0 of the slab is the stack's
     else:  # the stack's frame 0, for the redundant selection
-        d_f0 = torch.empty((1, Y, X), dtype=torch.int16, device="cuda")
-        lfm.synth_device(d_f0, X, Y, 1, T, z0=0, seed=SEED)
+        sel_frame = torch.empty((1, Y, X), dtype=torch.int16, device="cuda")
+        lfm.synth_device(sel_frame, X, Y, 1, T, z0=0, seed=SEED)
     torch.cuda.synchronize()
     enc = lfm.Encoder(device=local, num_threads=threads)
     shm = None
@@ -260,11 +260,9 @@ def main():
 
     place_ms = []
 
-    def finish(ticket, sel_ms, stats):
+    def finish(ticket, stats):
         # the .lfm stays in the encoder's buffer (no copy into a Python bytes object)
         b, st = enc.wait(ticket, copy=False)
-        st["select_ms"] = sel_ms
-        st["total_ms"] += sel_ms
         if shm is not None:
             t1 = time.perf_counter()
             place_in_shared(shm, b, rank, world, world * zf, backend, threads)
@@ -279,14 +277,14 @@ def main():
         pending = None
         b = None
         for _ in range(nsteps):
-            t0 = time.perf_counter()
-            k, _ = lfm.select_device(d_f0, X, Y, T, FAMILY)  # selection on the stack's frame 0
-            sel_ms = (time.perf_counter() - t0) * 1e3
-            ticket = enc.submit(d_img, z0, header_version=forced_request(k), nnum=T)
+            # auto request: the submit selects on the stack's frame 0 (its own
+            # frame 0 at rank 0, handed in on the others) on the encoder's
+            # stream, after the previous encode's kernels
+            ticket = enc.submit(d_img, z0, header_version=0, nnum=T, select_frame=sel_frame)
             if pending is not None:
-                b = finish(*pending, stats)
-            pending = (ticket, sel_ms)
-        return finish(*pending, stats) if pending is not None else None
+                b = finish(pending, stats)
+            pending = ticket
+        return finish(pending, stats) if pending is not None else None
 
     run(args.warmup, [])
     if world > 1:
@@ -302,8 +300,7 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0)
     # one unpipelined encode (select + encode + every copy, nothing in flight), for its latency
     t1 = time.perf_counter()
-    k1, _ = lfm.select_device(d_f0, X, Y, T, FAMILY)
-    enc.wait(enc.submit(d_img, z0, header_version=forced_request(k1), nnum=T), copy=False)
+    enc.wait(enc.submit(d_img, z0, header_version=0, nnum=T, select_frame=sel_frame), copy=False)
     latency_ms = max_over_ranks(time.perf_counter() - t1) * 1e3
 
     px_rank = X * Y * zf

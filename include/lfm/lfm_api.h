@@ -82,8 +82,22 @@ LFM_API int lfm_encoder_submit(lfm_encoder* enc, const void* img, int img_is_dev
                                uint32_t z0, const uint32_t xyzct[KLB_DATA_DIMS], int dataType, int headerVersion,
                                int Nnum, const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
                                const char metadata[KLB_METADATA_SIZE], uint64_t* ticket);
+/* lfm_encoder_submit with the frame auto-selection runs on: select_frame
+ * (X*Y samples, host or device like img) is the whole stack's frame 0 when img
+ * is a z-slab of it (z0 > 0), so every slab selects what the whole-stack
+ * encode selects (klb_imageIO.cpp:2316-2360); NULL = img's own frame 0.  An
+ * auto request (headerVersion & 0x7F < 8) on a slab with z0 > 0 needs it
+ * (returns 3 otherwise).  Selection then runs inside the submit, on the
+ * encoder's high-priority stream, after the previous encode's kernels. */
+LFM_API int lfm_encoder_submit_select(lfm_encoder* enc, const void* img, int img_is_device, const void* prev_frame,
+                                      uint32_t z0, const void* select_frame, const uint32_t xyzct[KLB_DATA_DIMS],
+                                      int dataType, int headerVersion, int Nnum,
+                                      const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                                      const char metadata[KLB_METADATA_SIZE], uint64_t* ticket);
 /* Wait for a submitted encode.  *out stays valid until the second submit
- * after it (or a synchronous encode on this encoder); returns its status. */
+ * after it (or a synchronous encode on this encoder); returns its status.
+ * On a nonzero status *out = NULL and *out_len = 0; 8 = the ticket was never
+ * submitted on this encoder or its buffer set has been reused since. */
 LFM_API int lfm_encoder_wait(lfm_encoder* enc, uint64_t ticket, const uint8_t** out, uint64_t* out_len,
                              lfm_encode_stats* stats);
 
@@ -123,7 +137,8 @@ LFM_API int lfm_place_slab(const uint8_t* slab, uint64_t slab_len, uint8_t* dst,
 /* Devices the writers farm block ranges to (klb_imageIO::writeImage,
  * writeKLBstack, writeLFMstack_c, lfm_encoder_encode_multi): n > 0 sets the
  * list (a device may repeat: several workers on one GPU); n = 0 restores the
- * default (env LFM_GPUS = "0,1,.." or a count, else every visible device).
+ * default (env LFM_GPUS = "0,1,.." or a count, else the current device in a one-process-per-GPU job (WORLD_SIZE /
+ * LOCAL_WORLD_SIZE > 1), else every visible device).
  * lfm_get_devices returns the count and fills up to cap entries. */
 LFM_API int lfm_set_devices(const int* devices, int n);
 LFM_API int lfm_get_devices(int* devices, int cap);

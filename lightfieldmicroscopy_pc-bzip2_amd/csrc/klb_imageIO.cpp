@@ -56,10 +56,13 @@ float klb_imageIO::bwt_entropy_2D(uint16_t* In, float* entropy, int is_src)
 {
     // klb_imageIO.cpp:2030-2093: 2D entropy of a device candidate buffer of
     // header.getImageSizePixels() symbols; candidate 0 (is_src == 0) is
-    // reported x0.96, the unscaled value is returned
+    // reported x0.96, the unscaled value is returned.  The reference multiplies
+    // the float by the DOUBLE literal 0.96 and stores the product back into a
+    // float (`*entropy = entropy_A*0.96`, klb_imageIO.cpp:2090): promote,
+    // multiply in double, round once -- e * 0.96f can differ in the last bit.
     float e = 0.f;
     if (lfm_hip_entropy2d(In, header.getImageSizePixels(), &e, nullptr) != LFM_HIP_OK) return -1.f;
-    if (entropy) *entropy = is_src != 0 ? e : e * 0.96f;
+    if (entropy) *entropy = is_src != 0 ? e : (float)((double)e * 0.96);
     return e;
 }
 

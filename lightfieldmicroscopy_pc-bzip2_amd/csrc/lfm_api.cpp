@@ -110,14 +110,33 @@ extern "C" int lfm_encoder_submit(lfm_encoder* e, const void* img, int img_is_de
     return e->enc.submit(img, img_is_device != 0, h, e->threads, &slab, ticket);
 }
 
+extern "C" int lfm_encoder_submit_select(lfm_encoder* e, const void* img, int img_is_device, const void* prev_frame,
+                                         uint32_t z0, const void* select_frame, const uint32_t xyzct[KLB_DATA_DIMS],
+                                         int dataType, int headerVersion, int Nnum,
+                                         const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,
+                                         const char metadata[KLB_METADATA_SIZE], uint64_t* ticket)
+{
+    if (!e || !img || !ticket) return 3;
+    klb_image_header h;
+    h.setHeader(xyzct, (KLB_DATA_TYPE)dataType, nullptr, blockSize, (KLB_COMPRESSION_TYPE)compressionType, metadata,
+                (uint8_t)headerVersion, (uint8_t)Nnum);
+    lfm::SlabSpec slab;
+    slab.z0 = z0;
+    slab.prev = prev_frame;
+    slab.select_frame = select_frame;
+    return e->enc.submit(img, img_is_device != 0, h, e->threads, &slab, ticket);
+}
+
 extern "C" int lfm_encoder_wait(lfm_encoder* e, uint64_t ticket, const uint8_t** out, uint64_t* out_len,
                                 lfm_encode_stats* stats)
 {
     if (!e || !out || !out_len) return 3;
     const lfm::PinnedBuffer* b = nullptr;
     const int rc = e->enc.wait(ticket, &b, stats);
-    *out = b ? b->data() : nullptr;
-    *out_len = b ? b->size() : 0;
+    // a failed encode leaves an earlier encode's bytes in that buffer set:
+    // hand out nothing rather than a stale .lfm
+    *out = (b && rc == 0) ? b->data() : nullptr;
+    *out_len = (b && rc == 0) ? b->size() : 0;
     return rc;
 }
 

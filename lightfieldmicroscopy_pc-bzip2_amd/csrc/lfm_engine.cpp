@@ -451,6 +451,7 @@ Encoder::~Encoder()
             if (d) (void)hipFree(d);
         if (d_ws_) (void)hipFree(d_ws_);
         if (d_prev_) (void)hipFree(d_prev_);
+        if (d_sel_) (void)hipFree(d_sel_);
         for (auto& set : bz_)
             for (BzSlot& sl : set) {
                 if (sl.d_ws) (void)hipFree(sl.d_ws);
@@ -558,6 +559,20 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         f.release();
         return f.rc;
     }
+    if (dev && dsym == (const uint8_t*)img) {
+        // no predictor stage (forced predictor 0, non-16-bit data): the symbols
+        // ARE the caller's image, which the caller may release or refill once
+        // submit returns -- the finisher must compress a copy of it
+        const size_t bytes = h.getImageSizeBytes();
+        if (!dev_alloc(d_sym_[p], d_sym_cap_[p], bytes) ||
+            hipMemcpyAsync(d_sym_[p], img, bytes, hipMemcpyDeviceToDevice, stream_) != hipSuccess ||
+            hipStreamSynchronize(stream_) != hipSuccess) {
+            f.rc = 3;
+            f.release();
+            return f.rc;
+        }
+        dsym = (const uint8_t*)d_sym_[p];
+    }
     if (trace) ts("predicted");
     auto hh = std::make_shared<klb_image_header>(h);
     f.th = std::thread([this, &f, hh, dsym, level, p, t0]() {
@@ -585,7 +600,7 @@ int Encoder::wait(uint64_t ticket, const PinnedBuffer** out, lfm_encode_stats* s
         if (st) *st = f.st;
         return f.rc;
     }
-    return 3;  // not submitted, or two submits ago
+    return kErrUnknownTicket;  // never submitted, already recycled (two submits ago), or 0
 }
 
 int Encoder::ensure_gpu()
@@ -600,7 +615,14 @@ int Encoder::ensure_gpu()
         if (hipGetDevice(&device_) != hipSuccess) device_ = 0;
     }
     if (device_ >= n || hipSetDevice(device_) != hipSuccess) return kErrNoGpu;
-    if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
+    // the predictor stage (selection + fused predictor) runs at the device's
+    // highest stream priority: a pipelined submit's short kernels then go ahead
+    // of the previous encode's GPU bzip2 work still queued on the other streams
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
+    if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_hi) != hipSuccess &&
+        hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess)
+        return kErrNoGpu;
     (void)hipEventCreate(&ev0_);
     (void)hipEventCreate(&ev1_);
     gpu_ready_ = true;
@@ -736,13 +758,28 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
             src = (const uint16_t*)d_in_;
         }
         if (v == 0 && autosel) {
-            // selection on frame 0 of volume (c=0, t=0) (klb_imageIO.cpp:2316-2360)
+            // selection on frame 0 of volume (c=0, t=0) (klb_imageIO.cpp:2316-2360),
+            // or on the whole stack's frame 0 handed in for a slab
             auto t0 = clk::now();
             const size_t need = lfm_hip_select_workspace_bytes((int)W, (int)H);
             if (!dev_alloc(d_ws_, d_ws_cap_, need)) return 3;
+            const uint16_t* sel = src;
+            if (slab.select_frame) {
+                if (dev) {
+                    sel = (const uint16_t*)slab.select_frame;
+                } else {
+                    if (!dev_alloc(d_sel_, d_sel_cap_, W * H * 2)) return 3;
+                    if (hipMemcpyAsync(d_sel_, slab.select_frame, W * H * 2, hipMemcpyHostToDevice, stream_) !=
+                        hipSuccess)
+                        return 3;
+                    sel = (const uint16_t*)d_sel_;
+                }
+            } else if (slab.z0 > 0) {
+                return 3;  // a slab's own frame 0 is not the stack's: the caller must hand that frame in
+            }
             float ent[8];
             int chosen = 0;
-            int rc = lfm_hip_select(src, (int)W, (int)H, T, fam, ent, &chosen, d_ws_, stream_);
+            int rc = lfm_hip_select(sel, (int)W, (int)H, T, fam, ent, &chosen, d_ws_, stream_);
             if (rc != LFM_HIP_OK) return 3;
             k = chosen;
             if (st) {
@@ -979,8 +1016,11 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                         if (hipHostMalloc(&h_sym_, bytes, hipHostMallocDefault) != hipSuccess) { rc = 3; break; }
                         h_sym_cap_ = bytes;
                     }
-                    if (hipMemcpyAsync(h_sym_, d_sym, bytes, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
-                        hipStreamSynchronize(stream_) != hipSuccess) {
+                    // on this batch's own HIP stream: stream_ belongs to the
+                    // caller thread's next submit (its predictor stage)
+                    hipStream_t fs = bz_[b % nslots].stream;
+                    if (hipMemcpyAsync(h_sym_, d_sym, bytes, hipMemcpyDeviceToHost, fs) != hipSuccess ||
+                        hipStreamSynchronize(fs) != hipSuccess) {
                         rc = 3;
                         break;
                     }

@@ -18,6 +18,7 @@ namespace lfm {
 // error codes beyond the reference's 2 / 3 / 5
 constexpr int kErrBadPredictor = 6;
 constexpr int kErrNoGpu = 7;
+constexpr int kErrUnknownTicket = 8;  // lfm_encoder_wait: ticket never submitted or already recycled
 
 bool gpu_bzip2_enabled();   // env LFM_GPU_BZIP2 (default on)
 bool gpu_decode_enabled();  // env LFM_GPU_DECODE (default on): inverse predictor on the GPU
@@ -104,10 +105,14 @@ int compress_blocks(const uint8_t* sym, klb_image_header& h, Sink& sink, int thr
 // bytes / 1e5)), klb_imageIO.cpp:108): a range of a larger stack codes at the
 // level of the whole stack's nominal block even when its own last block layer
 // is shallower.
+// select_frame: the frame auto-selection runs on (host or device like the
+// image) instead of the image's own frame 0 -- the whole stack's frame 0 when
+// this encode is a slab of it (klb_imageIO.cpp:2316-2360 selects on frame 0).
 struct SlabSpec {
     uint32_t z0 = 0;
     const void* prev = nullptr;
     int level = -1;
+    const void* select_frame = nullptr;
 };
 
 // clamp the block size to the dims and check the types (klb_imageIO.cpp:2402-2404)
@@ -186,6 +191,7 @@ private:
     void* d_sym_[2] = {nullptr, nullptr}; size_t d_sym_cap_[2] = {0, 0};  // by buffer set
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;
     void* d_prev_ = nullptr; size_t d_prev_cap_ = 0;
+    void* d_sel_ = nullptr; size_t d_sel_cap_ = 0;  // host select_frame uploaded
     // GPU bzip2 pipeline slots (stream, workspace, device + pinned output),
     // kBzSlots per buffer set (LFM_BZ2_SLOTS picks how many run, at most that)
     static constexpr int kBzSlots = 4;
@@ -206,7 +212,9 @@ Encoder& pooled_encoder(int dev, int slot, std::unique_lock<std::mutex>& lock);
 void release_pooled_encoders();
 
 // devices the writer farms block ranges to: lfm_set_devices, else env
-// LFM_GPUS ("0,1,2" or a count), else every visible device
+// LFM_GPUS ("0,1,2" or a count), else the current device when the process is one
+// rank of a one-process-per-GPU job (WORLD_SIZE / LOCAL_WORLD_SIZE > 1), else
+// every visible device
 std::vector<int> encode_devices();
 void set_encode_devices(const std::vector<int>& devs);
 

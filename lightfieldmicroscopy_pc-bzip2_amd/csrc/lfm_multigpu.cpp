@@ -84,6 +84,17 @@ std::vector<int> encode_devices()
         }
         if (!out.empty()) return out;
     }
+    // a process of a one-process-per-GPU job (torchrun / MPI launchers set
+    // these) owns its current device only: farming to every GPU of the node
+    // from each rank would oversubscribe them all
+    for (const char* v : {"LOCAL_WORLD_SIZE", "WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE"}) {
+        const char* e = std::getenv(v);
+        if (e && std::atoi(e) > 1) {
+            int dev = 0;
+            if (n <= 0 || hipGetDevice(&dev) != hipSuccess) dev = 0;
+            return {dev};
+        }
+    }
     for (int i = 0; i < n; ++i) out.push_back(i);
     return out;
 }
@@ -139,29 +150,10 @@ int encode_multi(const void* img, klb_image_header& h, Sink& sink, lfm_encode_st
     if (threads <= 0) threads = default_threads();
     if (st) std::memset(st, 0, sizeof(*st));
 
-    // predictor selection once, on frame 0 of volume (0,0) (klb_imageIO.cpp:2316-2360),
-    // then forced (request 8 + k) for every range
-    uint8_t hv = h.headerVersion;
-    const int req = hv & 0x7F;
-    const bool predictable = bpp == 2 && h.Nnum > 0;
-    if (predictable && req < NUM_PREDICTORS) {
-        auto ts = clk::now();
-        std::unique_lock<std::mutex> lk;
-        Encoder& e0 = pooled_encoder(devs[0], 0, lk);
-        int k = 0;
-        float ent[8] = {0};
-        if (int rc = e0.select_host_frame(img, (int)h.xyzct[0], (int)h.xyzct[1], h.Nnum, current_family(), &k, ent))
-            return rc;
-        hv = (uint8_t)((hv & 0x80) | (8 + k));
-        if (st) {
-            st->select_ms = ms_since(ts);
-            std::memcpy(st->entropy, ent, sizeof(ent));
-        }
-    }
-
     struct Work {
         uint64_t first, count;  // along the axis
         int dev, slot;
+        Encoder* enc = nullptr;
         int rc = -1;
         bool done = false, consumed = false;
         lfm_encode_stats st{};
@@ -176,14 +168,48 @@ int encode_multi(const void* img, klb_image_header& h, Sink& sink, lfm_encode_st
         work[w].dev = devs[w];
         work[w].slot = slots[devs[w]]++;
     }
+    // Every pooled encoder this call uses is locked here, by the calling
+    // thread, in one global (device, slot) order and held until the workers
+    // are joined: two concurrent calls whose device lists differ in order
+    // can then never hold one entry each while waiting for the other's.
+    std::vector<int> order(nw);
+    for (int w = 0; w < nw; ++w) order[w] = w;
+    std::sort(order.begin(), order.end(), [&](int a, int b) {
+        return std::make_pair(work[a].dev, work[a].slot) < std::make_pair(work[b].dev, work[b].slot);
+    });
+    std::vector<std::unique_lock<std::mutex>> held(nw);
+    for (int w : order) work[w].enc = &pooled_encoder(work[w].dev, work[w].slot, held[w]);
+
+    // predictor selection once, on frame 0 of volume (0,0) (klb_imageIO.cpp:2316-2360),
+    // then forced (request 8 + k) for every range.  It runs on the caller's
+    // thread with devs[0] current; the caller's device is restored after.
+    uint8_t hv = h.headerVersion;
+    const int req = hv & 0x7F;
+    const bool predictable = bpp == 2 && h.Nnum > 0;
+    if (predictable && req < NUM_PREDICTORS) {
+        auto ts = clk::now();
+        int caller_dev = -1;
+        if (hipGetDevice(&caller_dev) != hipSuccess) caller_dev = -1;
+        Encoder& e0 = *work[0].enc;  // (devs[0], slot 0)
+        int k = 0;
+        float ent[8] = {0};
+        const int src = e0.select_host_frame(img, (int)h.xyzct[0], (int)h.xyzct[1], h.Nnum, current_family(), &k, ent);
+        if (caller_dev >= 0) (void)hipSetDevice(caller_dev);
+        if (src) return src;
+        hv = (uint8_t)((hv & 0x80) | (8 + k));
+        if (st) {
+            st->select_ms = ms_since(ts);
+            std::memcpy(st->entropy, ent, sizeof(ent));
+        }
+    }
+
     std::mutex mu;
     std::condition_variable cv;
     const int wthreads = std::max(1, threads / nw);
     const int level = bzip2_level(h);  // the whole stack's nominal block (klb_imageIO.cpp:108)
     auto worker = [&](int w) {
         Work& W = work[w];
-        std::unique_lock<std::mutex> hold;  // this worker's encoder, until the writer consumed its output
-        Encoder& enc = pooled_encoder(W.dev, W.slot, hold);
+        Encoder& enc = *W.enc;  // locked by the calling thread until every worker is joined
         klb_image_header hs(h);
         hs.headerVersion = hv;
         hs.xyzct[axis] = (uint32_t)W.count;

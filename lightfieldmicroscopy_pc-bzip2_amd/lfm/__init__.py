@@ -37,7 +37,7 @@ EXPORTS = [
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
     "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_set_devices", "lfm_get_devices",
     "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab", "lfm_encoder_submit",
-    "lfm_encoder_wait",
+    "lfm_encoder_submit_select", "lfm_encoder_wait",
     # lfm_hip.h
     "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
@@ -104,6 +104,9 @@ def lib():
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
     L.lfm_encoder_submit.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_uint32, u32p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, u32p, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)]
+    L.lfm_encoder_submit_select.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_uint32, vp, u32p, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, u32p, ctypes.c_int, ctypes.c_char_p,
+                                            ctypes.POINTER(ctypes.c_uint64)]
     L.lfm_encoder_wait.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                    ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(EncodeStats)]
     L.lfm_encoder_encode_multi.argtypes = [vp, vp, u32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32p,
@@ -163,7 +166,8 @@ def require_gpu():
 
 def set_devices(devices=None):
     """Devices the writers farm block ranges to (lfm_set_devices); None or []
-    restores the default (env LFM_GPUS, else every visible device)."""
+    restores the default (env LFM_GPUS, else the current device inside a
+    WORLD_SIZE > 1 job, else every visible device)."""
     devices = list(devices or [])
     arr = (ctypes.c_int * max(1, len(devices)))(*devices)
     _check(lib().lfm_set_devices(arr, len(devices)), "lfm_set_devices")
@@ -340,22 +344,30 @@ class Encoder:
         return ctypes.string_at(out, n.value), st.as_dict()
 
     def submit(self, img, z0=0, prev=None, header_version=0, nnum=13, block_size=None, compression=1,
-               metadata=None, xyzct=None, data_type=None):
+               metadata=None, xyzct=None, data_type=None, select_frame=None):
         """Pipelined encode (lfm_encoder_submit) of a stack (z0 = 0) or a z-slab:
         returns a ticket once every kernel has run (img may be released); the
         .lfm's last payload copies finish in the background.  wait(ticket)
-        gives (.lfm, stats); at most two encodes are in flight."""
+        gives (.lfm, stats); at most two encodes are in flight.
+        select_frame: the frame auto-selection runs on (the whole stack's frame
+        0 for a slab; lfm_encoder_submit_select), same residency as img."""
         ptr, dev, xyzct, data_type, keep = self._operand(img, xyzct, data_type)
         pptr = None
         if prev is not None:
             pptr, pdev, _, _, pkeep = self._operand(prev, [1, 1, 1, 1, 1], data_type)
             if pdev != dev:
                 raise LfmError("prev must live where img lives (host or device)")
+        sptr = None
+        if select_frame is not None:
+            sptr, sdev, _, _, skeep = self._operand(select_frame, [1, 1, 1, 1, 1], data_type)
+            if sdev != dev:
+                raise LfmError("select_frame must live where img lives (host or device)")
         t = ctypes.c_uint64()
-        rc = lib().lfm_encoder_submit(self._h, ptr, dev, pptr, int(z0), _u32(xyzct), data_type, int(header_version),
-                                      int(nnum), _u32(block_size) if block_size is not None else None, compression,
-                                      _meta(metadata), ctypes.byref(t))
-        _check(rc, "lfm_encoder_submit")
+        rc = lib().lfm_encoder_submit_select(self._h, ptr, dev, pptr, int(z0), sptr, _u32(xyzct), data_type,
+                                             int(header_version), int(nnum),
+                                             _u32(block_size) if block_size is not None else None, compression,
+                                             _meta(metadata), ctypes.byref(t))
+        _check(rc, "lfm_encoder_submit_select")
         del keep
         return t.value
 

@@ -12,9 +12,21 @@ the expression the oracle builds for the same case from its formula table and
 temporal rule.  Python's `+ - >>` precedence equals C's, so equal parse trees
 mean equal integer arithmetic.
 
+Second check (check_case_conditions): the comparison above pairs the
+reference's i-th `out = ...` statement with the oracle's case
+(i // 16, i // 4 % 4, i % 4) = (z flag, tile case, position case).  That
+pairing is only right if the oracle classifies a pixel into the case whose
+reference branch conditions it satisfies.  So every reference branch path
+(`z==0`, `tx==0&&ty==0`, `u==0`, `v>0`, ... and their negations) is evaluated
+on every pixel of a 3 x 3-lens neighbourhood (T = 5) in both modes, and the
+ONE path it satisfies must be the one the oracle's exported tile_case /
+pos_case (lfmo_tile_case / lfmo_pos_case) select.  A permuted case order in
+the oracle -- consistent across all 21 tables, which the first check would
+miss -- fails here (tests/test_oracle.py mutation tests).
+
 Usage: python oracle/audit_tables.py [/root/reference]
 Exit status 0 when all 672 cases (3 families x 7 predictors x 2 modes x 16
-cases) agree.
+cases) agree and every sampled pixel lands on its case.
 """
 import ast
 import ctypes
@@ -156,6 +168,70 @@ def reference_table(ref_root):
     return table
 
 
+def reference_paths(ref_root):
+    """{(family, k): [32 branch paths]}: the full condition list (guard
+    included) of each `out[...] = ...` statement, in source order."""
+    paths = {}
+    for fam, fname in FAMILIES:
+        src = open(os.path.join(ref_root, "src", fname)).read()
+        for k in range(1, 8):
+            body = _strip_comments(_kernel_body(src, "_predictor%d_%s" % (k, fam)))
+            items, _ = _parse_block(body, 0)
+            rows = []
+            _walk(items, [], rows)
+            paths[(fam, k)] = [p for p, st in rows if st.startswith("out")]
+    return paths
+
+
+_COND_NAMES = {"z", "tx", "ty", "u", "v", "x", "y", "tileSize", "width", "height"}
+_COND_NODES = (ast.Expression, ast.BoolOp, ast.And, ast.Or, ast.UnaryOp, ast.Not, ast.Compare, ast.Eq, ast.NotEq,
+               ast.Lt, ast.LtE, ast.Gt, ast.GtE, ast.Name, ast.Load, ast.Constant)
+
+
+def _condition(c):
+    """A reference branch condition (C text) as a checked Python expression
+    code object: only comparisons / and / or / not over the kernel's index
+    variables and integer constants are accepted (the text is never executed
+    in any other form)."""
+    py = re.sub(r"!(?!=)", " not ", c.replace("&&", " and ").replace("||", " or "))
+    tree = ast.parse(py.strip(), mode="eval")
+    for node in ast.walk(tree):
+        if not isinstance(node, _COND_NODES):
+            raise ValueError("unexpected construct in reference condition %r" % c)
+        if isinstance(node, ast.Name) and node.id not in _COND_NAMES:
+            raise ValueError("unknown name %r in reference condition %r" % (node.id, c))
+        if isinstance(node, ast.Constant) and not isinstance(node.value, int):
+            raise ValueError("non-integer constant in reference condition %r" % c)
+    return compile(tree, "<reference condition>", "eval")
+
+
+def check_case_conditions(ref_root, tile_case, pos_case, T=5, paths=None):
+    """(pixels checked, mismatches): for every kernel and every pixel of the
+    lenses (tx, ty) in {0,1,2}^2, both modes, the index of the ONE reference
+    branch path the pixel satisfies must equal
+    z * 16 + tile_case(tx, ty) * 4 + pos_case(u, v)."""
+    paths = paths or reference_paths(ref_root)
+    compiled = {}
+    bad = []
+    n = 0
+    for (fam, k), plist in sorted(paths.items()):
+        code = [[compiled.setdefault(c, _condition(c)) for c in p] for p in plist]
+        for z in (0, 1):
+            for tx in range(3):
+                for ty in range(3):
+                    for u in range(T):
+                        for v in range(T):
+                            env = {"z": z, "tx": tx, "ty": ty, "u": u, "v": v, "x": u + tx * T, "y": v + ty * T,
+                                   "tileSize": T, "width": 1 << 20, "height": 1 << 20}
+                            hits = [i for i, p in enumerate(code)
+                                    if all(eval(c, {"__builtins__": {}}, env) for c in p)]
+                            exp = z * 16 + tile_case(tx, ty) * 4 + pos_case(u, v)
+                            n += 1
+                            if hits != [exp]:
+                                bad.append((fam, k, z, tx, ty, u, v, hits, exp))
+    return n, bad
+
+
 def oracle_formulas():
     """formula id -> expression text, parsed from lfm_oracle.c."""
     src = open(os.path.join(HERE, "lfm_oracle.c")).read()
@@ -182,9 +258,14 @@ def oracle_expression(lib, texts, fam_idx, k, zflag, tc, uc):
     return "((I-(%s))+P)>>1" % pred
 
 
-def audit(ref_root, lib_path=None):
+def audit_conditions(ref_root, lib_path=None):
     lib = ctypes.CDLL(lib_path or os.path.join(HERE, "liblfm_oracle.so"))
-    texts = oracle_formulas()
+    return check_case_conditions(ref_root, lib.lfmo_tile_case, lib.lfmo_pos_case)
+
+
+def audit(ref_root, lib_path=None, texts=None):
+    lib = ctypes.CDLL(lib_path or os.path.join(HERE, "liblfm_oracle.so"))
+    texts = texts or oracle_formulas()
     ref = reference_table(ref_root)
     bad = []
     n = 0
@@ -207,4 +288,8 @@ if __name__ == "__main__":
     for b in bad:
         print("MISMATCH fam=%s P%d z=%d tc=%d uc=%d\n  ref:    %s\n  oracle: %s" % b)
     print("audited %d cases, %d mismatches" % (n, len(bad)))
-    sys.exit(1 if bad else 0)
+    nc, badc = audit_conditions(root)
+    for b in badc[:20]:
+        print("CASE MISMATCH fam=%s P%d z=%d tx=%d ty=%d u=%d v=%d: reference path(s) %s, oracle case %d" % b)
+    print("checked %d pixels against the reference branch conditions, %d mismatches" % (nc, len(badc)))
+    sys.exit(1 if bad or badc else 0)

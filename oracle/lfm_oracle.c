@@ -246,6 +246,11 @@ static inline int pos_case(int u, int v)
     return v == 0 ? 2 : 3;
 }
 
+/* exported for audit_tables.py: the (tile case, position case) a pixel gets,
+ * checked there against the reference kernels' own branch conditions */
+int lfmo_tile_case(int tx, int ty) { return tile_case(tx, ty); }
+int lfmo_pos_case(int u, int v) { return pos_case(u, v); }
+
 /* Full-precision residual (int) of one pixel, before the int16 store.
  * Spatial: r = I - pred.  Temporal (zflag):
  *   tiles  r = I - ((pred + P) >> 1)          e.g. lfm_Predictors.cu:131-193

@@ -16,7 +16,12 @@
 //    readImageFull) -> compared with the input
 // 4. readKLBroiInPlace of a corner ROI -> compared with the crop
 // 5. readKLBheader fields
+// 6. the public selection helpers of klb_imageIO (src/klb_imageIO.h:91,101):
+//    bwt_entropy_2D on a device copy of frame 0 -- candidate 0 (is_src 0) is
+//    reported as (float)(e * 0.96) with 0.96 a double (klb_imageIO.cpp:2090);
+//    predict_and_2DEntropy over the 8 candidates
 // Prints one line per check; exit 0 only if every check passed.
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -26,6 +31,14 @@
 
 #include "klb_Cwrapper.h"
 #include "klb_imageIO.h"
+#include "lfm_api.h"
+#include "lfm_hip.h"
+
+// HIP runtime entry points (C linkage in libamdhip64) for the device buffers
+// the selection helpers take; declared here so this caller builds with g++
+extern "C" int hipMalloc(void** p, size_t n);
+extern "C" int hipMemcpy(void* dst, const void* src, size_t n, int kind);
+extern "C" int hipFree(void* p);
 
 static int failures = 0;
 static void check(bool ok, const char* what)
@@ -132,6 +145,45 @@ int main(int argc, char** argv)
         char rmeta[KLB_METADATA_SIZE];
         check(readKLBheader(klb.c_str(), rx, &dt, rps, rb, &ct, rmeta) == 0 && rx[0] == X && rb[0] == std::min(96u, X),
               "readKLBheader");
+    }
+    // 6. selection helpers on frame 0 (device buffers)
+    {
+        klb_imageIO io(mex);
+        io.header.setHeader(xyzct, UINT16_TYPE, ps, nullptr, BZIP2, meta);
+        io.header.xyzct[2] = 1;  // one frame, as writeImage's selection (klb_imageIO.cpp:2319-2327)
+        io.header.Nnum = 13;
+        const size_t fp = (size_t)X * Y;
+        uint16_t* d_in = nullptr;
+        uint16_t* d_c[8] = {nullptr};
+        bool ok = hipMalloc((void**)&d_in, fp * 2) == 0 && hipMemcpy(d_in, img.data(), fp * 2, 1) == 0;
+        for (int k = 0; k < 8 && ok; ++k) ok = hipMalloc((void**)&d_c[k], fp * 2) == 0;
+        check(ok, "device buffers for the selection helpers");
+        if (ok) {
+            float raw = 0.f, scaled = 0.f, src = 0.f;
+            const float r0 = io.bwt_entropy_2D(d_in, &scaled, 0);
+            const float r1 = io.bwt_entropy_2D(d_in, &src, 1);
+            raw = r0;
+            check(r0 >= 0.f && r0 == r1 && src == raw, "bwt_entropy_2D is_src 1 reports the unscaled entropy");
+            check(scaled == (float)((double)raw * 0.96), "bwt_entropy_2D is_src 0 reports (float)(e * 0.96) in double");
+            std::printf("INFO bwt_entropy_2D raw %.9g scaled %.9g (float-literal product %.9g)\n", raw, scaled,
+                        raw * 0.96f);
+            float ent[8] = {0};
+            std::atomic<uint64_t> next(0);
+            check(io.predict_and_2DEntropy(d_in, d_c, ent, &next, 8) == 0, "predict_and_2DEntropy rc 0");
+            float sel[8] = {0};
+            int chosen = -1;
+            check(lfm_hip_select(d_in, (int)X, (int)Y, 13, lfm_get_family(), sel, &chosen, nullptr, nullptr) == 0,
+                  "lfm_hip_select rc 0");
+            bool same = true;
+            for (int k = 0; k < 8; ++k) same &= ent[k] == sel[k];
+            check(same && ent[0] == scaled, "predict_and_2DEntropy entropies equal lfm_hip_select's");
+            std::printf("INFO entropies");
+            for (int k = 0; k < 8; ++k) std::printf(" %.9g", ent[k]);
+            std::printf(" chosen %d\n", chosen);
+        }
+        for (int k = 0; k < 8; ++k)
+            if (d_c[k]) (void)hipFree(d_c[k]);
+        if (d_in) (void)hipFree(d_in);
     }
     std::printf("%s: %d failure(s)\n", failures ? "FAILED" : "PASSED", failures);
     return failures ? 1 : 0;

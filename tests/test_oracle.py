@@ -31,6 +31,39 @@ def test_audit_tables_against_reference_text(oracle):
     assert bad == []
 
 
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REFERENCE, "src")), reason="reference tree absent")
+def test_audit_case_conditions_against_reference_text(oracle):
+    """Every pixel of a 3x3-lens neighbourhood, both modes, satisfies exactly
+    the reference branch path the oracle's tile_case / pos_case pick."""
+    import audit_tables
+    n, bad = audit_tables.audit_conditions(REFERENCE)
+    assert n == 21 * 2 * 9 * 25
+    assert bad == []
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REFERENCE, "src")), reason="reference tree absent")
+def test_audit_catches_mutations(oracle):
+    """The audit is not vacuous: a permuted position-case or tile-case order
+    (consistent over all 21 tables, invisible to the expression comparison)
+    and a changed operator in one formula each fail it."""
+    import audit_tables
+    lib = oracle.lib()
+    paths = audit_tables.reference_paths(REFERENCE)
+    swap_uc = {0: 1, 1: 0, 2: 2, 3: 3}
+    _, bad = audit_tables.check_case_conditions(REFERENCE, lib.lfmo_tile_case,
+                                                lambda u, v: swap_uc[lib.lfmo_pos_case(u, v)], paths=paths)
+    assert bad
+    swap_tc = {0: 0, 1: 2, 2: 1, 3: 3}
+    _, bad = audit_tables.check_case_conditions(REFERENCE, lambda tx, ty: swap_tc[lib.lfmo_tile_case(tx, ty)],
+                                                lib.lfmo_pos_case, paths=paths)
+    assert bad
+    texts = dict(audit_tables.oracle_formulas())
+    victim = next(i for i, t in texts.items() if "+" in t)
+    texts[victim] = texts[victim].replace("+", "-", 1)
+    _, bad = audit_tables.audit(REFERENCE, texts=texts)
+    assert bad
+
+
 def test_audit_kernel_tables_match_oracle_tables(oracle):
     """The product's own case tables (lfm_cases.h) equal the oracle's."""
     import re
