@@ -309,7 +309,9 @@ def main():
     alg_bytes = px_rank * 4  # 2 B read + 2 B written per pixel (no temporal frames in this config)
     achieved = alg_bytes / (pred_ms / 1e3) / 1e9
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "r02_traffic_predict.json")
+    tpath = os.path.join(REPO, "profiles", "r03_traffic_predict.json")
+    if not os.path.exists(tpath):
+        tpath = os.path.join(REPO, "profiles", "r02_traffic_predict.json")
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
@@ -336,8 +338,9 @@ def main():
                    "parallelism": "z-slab per GPU (slab-size all_gather only)", "host_threads_per_gpu": threads},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                     "kernel": "lfm::predict_ring<1,K,4,1,3> (fused angle predictor + symbolize, %d frames per "
-                               "launch)" % zf,
+                     "kernel": "lfm::predict_vec<1,K,15,1,4,1,3> (fused angle predictor + symbolize, 8 pixels "
+                               "per lane, %d frames per launch)" % zf,
+                     "traffic_file": os.path.relpath(tpath, REPO) if traffic is not None else None,
                      "kernel_ms": round(pred_ms, 4), "algorithmic_bytes": alg_bytes,
                      "read_only_frac": round(px_rank * 2 / (pred_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
         "stages_ms": {k: round(float(np.mean([s[k] for s in stats])), 3)

@@ -181,6 +181,13 @@ __host__ __device__ __forceinline__ uint32_t symbolize16(int r)
     return (uint32_t)(2 * a + (v >> 31)) & 0xFFFFu;
 }
 
+// the same symbol as a zig-zag of the low 16 bits: (r << 1) ^ (bit 15 of r
+// ? all ones : 0), masked to 16 bits -- 3 integer ops instead of abs + add
+__host__ __device__ __forceinline__ uint32_t zigzag16(int r)
+{
+    return ((uint32_t)r << 1 ^ (uint32_t)((r << 16) >> 31)) & 0xFFFFu;
+}
+
 __host__ __device__ __forceinline__ int unsymbolize16(uint32_t s)
 {
     int neg = (int)(s & 1u);

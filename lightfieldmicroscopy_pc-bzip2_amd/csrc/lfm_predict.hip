@@ -5,7 +5,13 @@
 // followed by symbolizeKernel (lfm_Predictors.cu:2769) and the per-frame
 // host<->device copies of Predictor_both (klb_imageIO.cpp:1244-1313).
 //
-// Fast kernel layout (W % 8 == 0, Nnum <= 31):
+// Main kernel (predict_vec, Nnum 13 / 15, W % 8 == 0; see its section): the
+// ring below with a lane owning 8 CONSECUTIVE pixels -- neighbours from 16-byte
+// LDS windows, packed 16-bit arithmetic for shift-free formulas, one 16-byte
+// symbol store per lane.  predict_ring (other Nnum <= 31) and predict_generic
+// (anything else) keep the layouts described next.
+//
+// Ring kernel layout (W % 8 == 0, Nnum <= 31):
 //   * one workgroup = NCW compute waves + 1 loader wave owns a 512-pixel strip
 //     of one frame and marches down a piece of its rows;
 //   * the loader wave streams rows HBM -> LDS with LDS-DMA
@@ -492,6 +498,450 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_cands(FrameSet p, int r
     }
 }
 
+// ---------------------------------------------------- vectorised ring path --
+// Nnum T in {13, 15}, W % 8 == 0.  Same loader wave / LDS ring / barrier
+// protocol as predict_ring, but a lane owns 8 CONSECUTIVE pixels of a row:
+//   * its neighbours come from three 16-byte LDS reads per ring row (the
+//     24-pixel window [x0 - 16, x0 + 8) holds every left reach <= T + 1 = 16),
+//     i.e. 3 ds_read_b128 per row instead of one ds_read_u16 per pixel and
+//     neighbour; the values are picked out of the window's dwords with
+//     compile-time shifts (T is a template parameter);
+//   * its 8 symbols leave as ONE 16-byte non-temporal store (1 KiB per wave
+//     instruction instead of 128 B).
+// A strip is SW = WPR * 512 pixels wide; WPR compute waves share each row
+// (wave w: row group w / WPR, quarter w % WPR), so SW = 2048 streams whole
+// 4 KiB rows per workgroup.
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+constexpr int kVHalo = 16;  // left halo pixels per ring slot (T + 1 <= 16)
+
+struct Win24 {  // pixels [x0 - 16, x0 + 8) of one ring row
+    uint32_t w[12];
+    template <int I>
+    __device__ __forceinline__ int px() const
+    {
+        static_assert(I >= 0 && I < 24, "window index");
+        return (int)((w[I >> 1] >> ((I & 1) * 16)) & 0xFFFFu);
+    }
+};
+
+// p: the lane's first pixel in the ring slot (16-byte aligned); blocks the
+// caller never reads are removed by the compiler
+__device__ __forceinline__ void load_win(const uint16_t* p, Win24& r)
+{
+    const v4u* q = (const v4u*)(p - 16);
+    const v4u a = q[0], b = q[1], c = q[2];
+    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;
+    r.w[4] = b.x; r.w[5] = b.y; r.w[6] = b.z; r.w[7] = b.w;
+    r.w[8] = c.x; r.w[9] = c.y; r.w[10] = c.z; r.w[11] = c.w;
+}
+
+// neighbours of pixel J of the lane's 8 (window index 16 + J - dx)
+template <int T, int J>
+struct VecNb {
+    const Win24& r0;   // row y
+    const Win24& r1;   // row y - 1
+    const Win24& rT;   // row y - T
+    const Win24& rT1;  // row y - T - 1
+    template <int N>
+    __device__ __forceinline__ int at() const
+    {
+        if constexpr (N == NB_A) return r0.template px<15 + J>();
+        if constexpr (N == NB_B) return r1.template px<16 + J>();
+        if constexpr (N == NB_C) return r1.template px<15 + J>();
+        if constexpr (N == NB_AP) return r0.template px<16 + J - T>();
+        if constexpr (N == NB_BP) return rT.template px<16 + J>();
+        if constexpr (N == NB_CP) return rT.template px<16 + J - T>();
+        if constexpr (N == NB_AP1) return r0.template px<15 + J - T>();
+        if constexpr (N == NB_BP1) return rT1.template px<16 + J>();
+        if constexpr (N == NB_ABP) return rT.template px<15 + J>();
+        if constexpr (N == NB_BAP) return r1.template px<16 + J - T>();
+        return 0;
+    }
+};
+
+struct VecRows {
+    Win24 r0, r1, rT, rT1;
+    uint32_t p[4];  // previous frame, pixels x0 .. x0+7 (temporal frames)
+    template <int J>
+    __device__ __forceinline__ int prev() const
+    {
+        return (int)((p[J >> 1] >> ((J & 1) * 16)) & 0xFFFFu);
+    }
+};
+
+// pixel J on a row y >= T of a full strip: tile case TC_XY except x < T (TC_0Y,
+// FIRST strip only); position case by (u == 0) per pixel and V0 per row
+template <int FAM, int K, int T, bool TEMP, bool V0, bool FIRST, int J>
+__device__ __forceinline__ uint32_t vec_fast_px(const VecRows& rw, uint32_t u0bits, int x0)
+{
+    constexpr int ucU = V0 ? UC_CORNER : UC_COL;
+    constexpr int ucI = V0 ? UC_ROW : UC_IN;
+    VecNb<T, J> g{rw.r0, rw.r1, rw.rT, rw.rT1};
+    const int I = rw.r0.template px<16 + J>();
+    const int P = TEMP ? rw.template prev<J>() : 0;
+    if constexpr (K == 0) return (uint32_t)(I + P) & 0xFFFFu;  // diagnostic: copy through the ring
+    const int m0 = -(int)((u0bits >> J) & 1u);
+    const int r_u = case_residual<FAM, K, TC_XY, ucU, TEMP>(g, I, P);
+    const int r_i = case_residual<FAM, K, TC_XY, ucI, TEMP>(g, I, P);
+    int res = r_i ^ ((r_u ^ r_i) & m0);
+    if constexpr (FIRST) {
+        if (x0 < T) {  // lanes of the first lens column (uniform per lane)
+            const int mt = -(int)(x0 + J < T);
+            const int t_u = case_residual<FAM, K, TC_0Y, ucU, TEMP>(g, I, P);
+            const int t_i = case_residual<FAM, K, TC_0Y, ucI, TEMP>(g, I, P);
+            const int rt = t_i ^ ((t_u ^ t_i) & m0);
+            res = res ^ ((rt ^ res) & mt);
+        }
+    }
+    return zigzag16(res);
+}
+
+// any pixel J (rows y < T): full per-pixel case logic
+template <int FAM, int K, int T, bool TEMP, int J>
+__device__ __forceinline__ uint32_t vec_slow_px(const VecRows& rw, int x0, int ty, int v)
+{
+    VecNb<T, J> g{rw.r0, rw.r1, rw.rT, rw.rT1};
+    const int I = rw.r0.template px<16 + J>();
+    const int P = TEMP ? rw.template prev<J>() : 0;
+    if constexpr (K == 0) return (uint32_t)(I + P) & 0xFFFFu;
+    const int x = x0 + J;
+    const int tx = x / T, u = x - tx * T;
+    return zigzag16(residual_any_case<FAM, K, TEMP>(g, tile_case(tx, ty), pos_case(u, v), I, P));
+}
+
+// ---- packed pairs: formulas without a shift ((A + B - C), B, Bp + Ap - Cp,
+// ...) are needed only mod 2^16 (the residual is stored as int16), so two
+// pixels go through each 32-bit register with packed 16-bit adds; the
+// symbol is the zig-zag (r << 1) ^ (r >> 15) of the int16 residual, which
+// equals 2|r| + (r >> 31) (lfm_Predictors.cu:16-26) including r = -32768.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_pk(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// pixels I, I+1 of a window as one packed register
+template <int I>
+__device__ __forceinline__ uint32_t win_pair(const Win24& r)
+{
+    static_assert(I >= 0 && I + 1 < 24, "window pair");
+    if constexpr ((I & 1) == 0) return r.w[I >> 1];
+    else return __builtin_amdgcn_alignbit(r.w[(I + 1) >> 1], r.w[I >> 1], 16);
+}
+
+template <int F>
+__host__ __device__ constexpr bool pk_formula()
+{
+    return F == F_Z || F == F_A || F == F_B || F == F_C || F == F_AP || F == F_BP || F == F_CP || F == F_ABC ||
+           F == F_BAC || F == F_ABC_SUM || F == F_P4_CORNER;
+}
+
+// neighbours of the pixel pair 2M, 2M+1 (window index 16 + 2M - dx)
+template <int T, int M>
+struct VecNbPk {
+    const Win24& r0;
+    const Win24& r1;
+    const Win24& rT;
+    const Win24& rT1;
+    template <int N>
+    __device__ __forceinline__ s16x2 at() const
+    {
+        if constexpr (N == NB_A) return as_pk(win_pair<15 + 2 * M>(r0));
+        if constexpr (N == NB_B) return as_pk(win_pair<16 + 2 * M>(r1));
+        if constexpr (N == NB_C) return as_pk(win_pair<15 + 2 * M>(r1));
+        if constexpr (N == NB_AP) return as_pk(win_pair<16 + 2 * M - T>(r0));
+        if constexpr (N == NB_BP) return as_pk(win_pair<16 + 2 * M>(rT));
+        if constexpr (N == NB_CP) return as_pk(win_pair<16 + 2 * M - T>(rT));
+        return s16x2{0, 0};
+    }
+};
+
+template <int F, class G>
+__device__ __forceinline__ s16x2 pk_eval(const G& g)
+{
+    static_assert(pk_formula<F>(), "formula has a shift: not exact in 16 bits");
+    if constexpr (F == F_Z) return s16x2{0, 0};
+    if constexpr (F == F_A) return g.template at<NB_A>();
+    if constexpr (F == F_B) return g.template at<NB_B>();
+    if constexpr (F == F_C) return g.template at<NB_C>();
+    if constexpr (F == F_AP) return g.template at<NB_AP>();
+    if constexpr (F == F_BP) return g.template at<NB_BP>();
+    if constexpr (F == F_CP) return g.template at<NB_CP>();
+    if constexpr (F == F_ABC || F == F_BAC) return g.template at<NB_A>() + g.template at<NB_B>() - g.template at<NB_C>();
+    if constexpr (F == F_ABC_SUM || F == F_P4_CORNER)
+        return g.template at<NB_BP>() + g.template at<NB_AP>() - g.template at<NB_CP>();
+    return s16x2{0, 0};
+}
+
+__device__ __forceinline__ uint32_t pk_zigzag(s16x2 r)
+{
+    const s16x2 one{1, 1}, fifteen{15, 15};
+    return as_u32(r << one) ^ as_u32(r >> fifteen);
+}
+
+// the row's formulas for (tile case, u == 0 / u > 0) are all shift-free
+template <int FAM, int K, bool TEMP, bool V0, bool FIRST>
+__host__ __device__ constexpr bool pk_row_ok()
+{
+    if constexpr (TEMP || K < 1) {
+        return false;
+    } else {
+        constexpr int ucU = V0 ? UC_CORNER : UC_COL, ucI = V0 ? UC_ROW : UC_IN;
+        return pk_formula<case_formula(FAM, K, TC_XY, ucU)>() && pk_formula<case_formula(FAM, K, TC_XY, ucI)>() &&
+               (!FIRST || (pk_formula<case_formula(FAM, K, TC_0Y, ucU)>() &&
+                           pk_formula<case_formula(FAM, K, TC_0Y, ucI)>()));
+    }
+}
+
+// per-lane masks of a packed pair: 0xFFFF in the half whose pixel has the bit
+__device__ __forceinline__ uint32_t pair_mask(uint32_t bits, int m)
+{
+    return (((bits >> (2 * m)) & 1u) ? 0xFFFFu : 0u) | (((bits >> (2 * m + 1)) & 1u) ? 0xFFFF0000u : 0u);
+}
+
+template <int FAM, int K, int T, bool V0, bool FIRST, int M>
+__device__ __forceinline__ uint32_t vec_pk_pair(const VecRows& rw, uint32_t u0bits, uint32_t firstbits, int x0)
+{
+    constexpr int ucU = V0 ? UC_CORNER : UC_COL, ucI = V0 ? UC_ROW : UC_IN;
+    VecNbPk<T, M> g{rw.r0, rw.r1, rw.rT, rw.rT1};
+    const s16x2 I = as_pk(win_pair<16 + 2 * M>(rw.r0));
+    const uint32_t mk = pair_mask(u0bits, M);
+    const uint32_t r_u = as_u32(I - pk_eval<case_formula(FAM, K, TC_XY, ucU)>(g));
+    const uint32_t r_i = as_u32(I - pk_eval<case_formula(FAM, K, TC_XY, ucI)>(g));
+    uint32_t res = (r_u & mk) | (r_i & ~mk);
+    if constexpr (FIRST) {
+        if (x0 < T) {
+            const uint32_t mt = pair_mask(firstbits, M);
+            const uint32_t t_u = as_u32(I - pk_eval<case_formula(FAM, K, TC_0Y, ucU)>(g));
+            const uint32_t t_i = as_u32(I - pk_eval<case_formula(FAM, K, TC_0Y, ucI)>(g));
+            const uint32_t rt = (t_u & mk) | (t_i & ~mk);
+            res = (rt & mt) | (res & ~mt);
+        }
+    }
+    return pk_zigzag(as_pk(res));
+}
+
+template <int FAM, int K, int T, bool TEMP, bool V0, bool FIRST>
+__device__ __forceinline__ v4u vec_fast_row(const VecRows& rw, uint32_t u0bits, int x0)
+{
+    if constexpr (pk_row_ok<FAM, K, TEMP, V0, FIRST>()) {
+        uint32_t firstbits = 0;
+        if constexpr (FIRST) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) firstbits |= (uint32_t)(x0 + j < T) << j;
+        }
+        v4u o;
+        o.x = vec_pk_pair<FAM, K, T, V0, FIRST, 0>(rw, u0bits, firstbits, x0);
+        o.y = vec_pk_pair<FAM, K, T, V0, FIRST, 1>(rw, u0bits, firstbits, x0);
+        o.z = vec_pk_pair<FAM, K, T, V0, FIRST, 2>(rw, u0bits, firstbits, x0);
+        o.w = vec_pk_pair<FAM, K, T, V0, FIRST, 3>(rw, u0bits, firstbits, x0);
+        return o;
+    }
+    v4u o;
+    o.x = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 0>(rw, u0bits, x0) |
+          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 1>(rw, u0bits, x0) << 16);
+    o.y = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 2>(rw, u0bits, x0) |
+          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 3>(rw, u0bits, x0) << 16);
+    o.z = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 4>(rw, u0bits, x0) |
+          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 5>(rw, u0bits, x0) << 16);
+    o.w = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 6>(rw, u0bits, x0) |
+          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 7>(rw, u0bits, x0) << 16);
+    return o;
+}
+
+template <int FAM, int K, int T, bool TEMP>
+__device__ __forceinline__ v4u vec_slow_row(const VecRows& rw, int x0, int ty, int v)
+{
+    v4u o;
+    o.x = vec_slow_px<FAM, K, T, TEMP, 0>(rw, x0, ty, v) | (vec_slow_px<FAM, K, T, TEMP, 1>(rw, x0, ty, v) << 16);
+    o.y = vec_slow_px<FAM, K, T, TEMP, 2>(rw, x0, ty, v) | (vec_slow_px<FAM, K, T, TEMP, 3>(rw, x0, ty, v) << 16);
+    o.z = vec_slow_px<FAM, K, T, TEMP, 4>(rw, x0, ty, v) | (vec_slow_px<FAM, K, T, TEMP, 5>(rw, x0, ty, v) << 16);
+    o.w = vec_slow_px<FAM, K, T, TEMP, 6>(rw, x0, ty, v) | (vec_slow_px<FAM, K, T, TEMP, 7>(rw, x0, ty, v) << 16);
+    return o;
+}
+
+// loader: row src_row of strip xs into ring slot slot_idx (WPR 1-KiB DMAs for
+// the strip + one for the 16-pixel left halo); P ring rows have no halo
+template <int WPR>
+__device__ __forceinline__ void vdma_row(uint16_t* ring, int slot_idx, const uint16_t* f, int W, int src_row, int xs,
+                                         int lane)
+{
+    constexpr int SW = WPR * 512;
+    uint16_t* slot = ring + slot_idx * (kVHalo + SW);
+    const uint16_t* srow = f + (size_t)src_row * W;
+#pragma unroll
+    for (int q = 0; q < WPR; ++q) {
+        const int x = min(xs + q * 512 + lane * 8, W - 8);
+        glds16(srow + x, slot + kVHalo + q * 512);
+    }
+    if (lane < kVHalo / 8) glds16(srow + (xs > 0 ? xs - kVHalo + lane * 8 : lane * 8), slot);
+}
+
+template <int WPR>
+__device__ __forceinline__ void vdma_prev_row(uint16_t* pring, int pslot_idx, const uint16_t* pf, int W, int src_row,
+                                              int xs, int lane)
+{
+    constexpr int SW = WPR * 512;
+    uint16_t* slot = pring + pslot_idx * SW;
+#pragma unroll
+    for (int q = 0; q < WPR; ++q) {
+        const int x = min(xs + q * 512 + lane * 8, W - 8);
+        glds16(pf + (size_t)src_row * W + x, slot + q * 512);
+    }
+}
+
+template <int WPR, int RS, bool TEMP>
+__device__ __forceinline__ void vdma_step(uint16_t* ring, int R, int slot0, uint16_t* pring, int RP, int pslot0,
+                                          const uint16_t* f, const uint16_t* pf, int W, int ys, int ye, int s, int xs,
+                                          int lane)
+{
+#pragma unroll
+    for (int i = 0; i < RS; ++i) {
+        const int src = min(ys + s * RS + i, ye - 1);
+        int si = slot0 + i;
+        si = si >= R ? si - R : si;
+        vdma_row<WPR>(ring, si, f, W, src, xs, lane);
+        if constexpr (TEMP) {
+            int pi = pslot0 + i;
+            pi = pi >= RP ? pi - RP : pi;
+            vdma_prev_row<WPR>(pring, pi, pf, W, src, xs, lane);
+        }
+    }
+}
+
+// One work item (frame, row piece, strip) of a vec workgroup: NCW compute
+// waves (row group w / WPR, quarter w % WPR) + one loader wave (wave NCW).
+template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD, bool TEMP>
+__device__ __forceinline__ void vec_item(const FrameSet& p, uint16_t* ring, int R, uint16_t* pring, int RP,
+                                         const uint16_t* f, const uint16_t* pf, uint16_t* outf, int xs, int ys, int ye,
+                                         int wave, int lane)
+{
+    constexpr int SW = WPR * 512;
+    constexpr int RG = NCW / WPR;  // rows computed side by side
+    constexpr int RS = RG * RPW;   // rows per step
+    constexpr int kLoadsPerStep = RS * (WPR + 1 + (TEMP ? WPR : 0));
+    constexpr int kWait = kLoadsPerStep * (PD - 1) < 63 ? kLoadsPerStep * (PD - 1) : 63;
+    static_assert(NCW % WPR == 0, "compute waves per row");
+    constexpr int slot = kVHalo + SW;
+    const bool loader = wave == NCW;
+    const int nsteps = (ye - ys + RS - 1) / RS;
+    auto adv = [](int v, int d, int m) { v += d; while (v >= m) v -= m; return v; };
+    auto wrap = [&](int s) { return s < 0 ? s + R : s; };
+    const int rg = wave / WPR, sub = wave - (wave / WPR) * WPR;
+    const int xl = sub * 512 + lane * 8;  // lane's first pixel in the strip
+    const int x0 = xs + xl;
+    const bool lane_in = x0 < p.W;
+    const bool full = xs + SW <= p.W;
+    uint32_t u0bits = 0;
+    int y = ys + rg, sy = 0, py = 0, vy = 0;
+    int lslot = 0, lpslot = 0;
+    if (!loader) {
+        const int u0 = x0 % T;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u0bits |= (uint32_t)(((u0 + j) % T) == 0) << j;
+        sy = y % R;
+        py = TEMP ? y % RP : 0;
+        vy = y % T;
+    } else {
+        const int r0 = max(0, ys - T - 1);
+        int ps = r0 % R;
+        for (int row = r0; row < ys; ++row) {
+            vdma_row<WPR>(ring, ps, f, p.W, row, xs, lane);
+            ps = ps + 1 == R ? 0 : ps + 1;
+        }
+        int slot0 = ys % R, pslot0 = TEMP ? ys % RP : 0;
+        for (int s = 0; s < PD && s < nsteps; ++s) {
+            vdma_step<WPR, RS, TEMP>(ring, R, slot0, pring, RP, pslot0, f, pf, p.W, ys, ye, s, xs, lane);
+            slot0 = adv(slot0, RS, R);
+            if (TEMP) pslot0 = adv(pslot0, RS, RP);
+        }
+        lslot = slot0;
+        lpslot = pslot0;
+    }
+    for (int s = 0; s < nsteps; ++s) {
+        if (loader) {
+            if (s + PD < nsteps) wait_vmcnt<kWait>();
+            else wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (loader) {
+            if (s + PD < nsteps) {
+                vdma_step<WPR, RS, TEMP>(ring, R, lslot, pring, RP, lpslot, f, pf, p.W, ys, ye, s + PD, xs, lane);
+                lslot = adv(lslot, RS, R);
+                if (TEMP) lpslot = adv(lpslot, RS, RP);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                if (y < ye && lane_in) {
+                    const int h = kVHalo + xl;
+                    VecRows rw;
+                    load_win(ring + sy * slot + h, rw.r0);
+                    load_win(ring + wrap(sy - 1) * slot + h, rw.r1);
+                    load_win(ring + wrap(sy - T) * slot + h, rw.rT);
+                    load_win(ring + wrap(sy - T - 1) * slot + h, rw.rT1);
+                    if constexpr (TEMP) {
+                        const v4u pv = *(const v4u*)(pring + py * SW + xl);
+                        rw.p[0] = pv.x; rw.p[1] = pv.y; rw.p[2] = pv.z; rw.p[3] = pv.w;
+                    }
+                    v4u o;
+                    if (y < T || !full) {
+                        o = vec_slow_row<FAM, K, T, TEMP>(rw, x0, y / T, vy);
+                    } else if (x0 < 512) {  // the strip that starts the frame: first lens column
+                        o = vy == 0 ? vec_fast_row<FAM, K, T, TEMP, true, true>(rw, u0bits, x0)
+                                    : vec_fast_row<FAM, K, T, TEMP, false, true>(rw, u0bits, x0);
+                    } else {
+                        o = vy == 0 ? vec_fast_row<FAM, K, T, TEMP, true, false>(rw, u0bits, x0)
+                                    : vec_fast_row<FAM, K, T, TEMP, false, false>(rw, u0bits, x0);
+                    }
+                    __builtin_nontemporal_store(o, (v4u*)(outf + (size_t)y * p.W + x0));
+                }
+                y += RG;
+                sy = adv(sy, RG, R);
+                if (TEMP) py = adv(py, RG, RP);
+                vy = adv(vy, RG, T);
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
+__global__ __launch_bounds__(NCW * 64 + 64) void predict_vec(FrameSet p, int rows_per_piece, int npiece, int nstrip,
+                                                             int xcd_map, int R, int RP)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    uint16_t* ring = lds;
+    uint16_t* pring = lds + R * (kVHalo + WPR * 512);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const size_t fs = (size_t)p.W * p.H;
+    const int b = blockIdx.x;
+    int strip, group;
+    if (xcd_map) {
+        const int q = b >> 3;
+        strip = q % nstrip;
+        group = (q / nstrip) * 8 + (b & 7);
+    } else {
+        strip = b % nstrip;
+        group = b / nstrip;
+    }
+    const int piece = group % npiece;
+    const int fz = group / npiece;
+    if (fz >= p.nz) return;
+    const int xs = strip * WPR * 512;
+    const int ys = piece * rows_per_piece;
+    const int ye = min(ys + rows_per_piece, p.H);
+    if (ys >= ye) return;
+    const uint16_t* f = p.in + (size_t)fz * fs;
+    uint16_t* outf = p.out + (size_t)fz * fs;
+    if (frame_temporal(p, fz))
+        vec_item<FAM, K, T, WPR, NCW, RPW, PD, true>(p, ring, R, pring, RP, f, frame_prev(p, fz), outf, xs, ys, ye,
+                                                     wave, lane);
+    else
+        vec_item<FAM, K, T, WPR, NCW, RPW, PD, false>(p, ring, R, pring, RP, f, nullptr, outf, xs, ys, ye, wave,
+                                                      lane);
+}
+
 // -------------------------------------------------------------- launchers --
 // NCW compute waves + 1 loader wave per workgroup; PD steps of NCW*RPW rows in
 // flight.  Ring rows live during a step: y-T-1 .. y+NCW*RPW-1 plus the PD
@@ -517,16 +967,19 @@ struct Plan {
 // re-reads only its T+1 priming rows, so fewer, taller pieces waste less
 // (1.5 % at 2048 rows / 3 pieces vs 6 % for 256-row segments).  Pieces stay
 // >= 2(T+1) rows.
-static hipError_t make_plan(const FrameSet& p, const void* fn, int ncw, int rpw, int pd, int copies, Plan& pl)
+// rs = rows per step, sw = strip width (pixels), halo = left halo pixels per slot
+static hipError_t make_plan_shape(const FrameSet& p, const void* fn, int threads, int rs, int pd, int sw, int halo,
+                                  int copies, Plan& pl)
 {
     const bool any_temporal = p.video && (p.nz > 1 || (p.z0 & 1));
-    pl.R = ncw * rpw * (pd + 1) + p.T + 1;
-    pl.RP = any_temporal ? ncw * rpw * (pd + 1) : 0;
-    pl.halo = p.T <= 15 ? 16 : 32;
-    pl.lds = ((size_t)pl.R * (pl.halo + kStrip) + (size_t)pl.RP * kStrip) * sizeof(uint16_t);
-    pl.nstrip = (p.W + kStrip - 1) / kStrip;
+    pl.R = rs * (pd + 1) + p.T + 1;
+    pl.RP = any_temporal ? rs * (pd + 1) : 0;
+    pl.halo = halo;
+    pl.lds = ((size_t)pl.R * (pl.halo + sw) + (size_t)pl.RP * sw) * sizeof(uint16_t);
+    pl.nstrip = (p.W + sw - 1) / sw;
+    const int ncw = rs;  // rows are padded to whole steps below
     int occ = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, ncw * 64 + 64, pl.lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, pl.lds);
     if (e != hipSuccess || occ <= 0) occ = 1;
     int dev = 0, ncu = 0;
     (void)hipGetDevice(&dev);
@@ -537,13 +990,18 @@ static hipError_t make_plan(const FrameSet& p, const void* fn, int ncw, int rpw,
     int npiece = std::max(1, resident / std::max(1, cols));
     npiece = std::min(npiece, std::max(1, p.H / (2 * (p.T + 1))));
     int rows = (p.H + npiece - 1) / npiece;
-    rows = (rows + ncw * rpw - 1) / (ncw * rpw) * (ncw * rpw);
+    rows = (rows + ncw - 1) / ncw * ncw;
     pl.rows_per_piece = rows;
     pl.npiece = (p.H + rows - 1) / rows;
     const int ngroups = p.nz * pl.npiece;
     pl.xcd_map = (ngroups % 8) == 0 && pl.nstrip > 1;
     pl.grid = ngroups * pl.nstrip;
     return hipSuccess;
+}
+
+static hipError_t make_plan(const FrameSet& p, const void* fn, int ncw, int rpw, int pd, int copies, Plan& pl)
+{
+    return make_plan_shape(p, fn, ncw * 64 + 64, ncw * rpw, pd, kStrip, p.T <= 15 ? 16 : 32, copies, pl);
 }
 
 static hipError_t launch_plan(const void* fn, FrameSet p, const Plan& pl, int ncw, int gy, hipStream_t st)
@@ -561,9 +1019,57 @@ static bool fast_ok(const FrameSet& p, int force_generic)
     return !force_generic && p.T <= kMaxFastT && (p.W % 8) == 0 && p.W >= 32;
 }
 
+// vectorised path shape per family (WPR waves per row = strip of WPR * 512
+// pixels, NCW compute waves, RPW rows per compute wave and step, PD steps of
+// prefetch).  Measured on config 3 (scripts/pred_probe.hip, profiles/r03_pred_probe*.jsonl):
+// angle / space run their (packed, shift-free) formulas at copy speed with
+// one 512-pixel strip, 4 compute waves, 3 steps ahead; the tiles formulas
+// (shifted sums, 32-bit) need more waves per CU to hide their VALU chains:
+// 1024-pixel strips, 8 compute waves (0.227 vs 0.251 ms, round-2 ring 0.236).
+template <int FAM>
+struct VecShape {
+    static constexpr int WPR = FAM == 0 ? 2 : 1;
+    static constexpr int NCW = FAM == 0 ? 8 : 4;
+    static constexpr int RPW = 1;
+    static constexpr int PD = 3;
+};
+
+static bool vec_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("LFM_PRED_VEC");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
+template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
+static hipError_t launch_vec_shape(const FrameSet& p, hipStream_t st)
+{
+    const void* fn = (const void*)predict_vec<FAM, K, T, WPR, NCW, RPW, PD>;
+    Plan pl;
+    hipError_t e = make_plan_shape(p, fn, NCW * 64 + 64, (NCW / WPR) * RPW, PD, WPR * 512, kVHalo, 1, pl);
+    if (e != hipSuccess) return e;
+    return launch_plan(fn, p, pl, NCW, 1, st);
+}
+
+template <int FAM, int K>
+static hipError_t launch_vec(const FrameSet& p, hipStream_t st)
+{
+    using S = VecShape<FAM>;
+    if (p.T == 15) return launch_vec_shape<FAM, K, 15, S::WPR, S::NCW, S::RPW, S::PD>(p, st);
+    return launch_vec_shape<FAM, K, 13, S::WPR, S::NCW, S::RPW, S::PD>(p, st);
+}
+
+static bool vec_ok(const FrameSet& p, int force_generic)
+{
+    return !force_generic && vec_enabled() && (p.T == 13 || p.T == 15) && (p.W % 8) == 0 && p.W >= 32;
+}
+
 template <int FAM, int K>
 static hipError_t launch_k(const FrameSet& p, hipStream_t st, int force_generic)
 {
+    if (vec_ok(p, force_generic)) return launch_vec<FAM, K>(p, st);
     if (!fast_ok(p, force_generic)) {
         size_t total = (size_t)p.W * p.H * p.nz;
         int grid = (int)std::min<size_t>((total + 255) / 256, 256 * 16);

@@ -148,6 +148,32 @@ __global__ __launch_bounds__(256) void k_band(const v4u* __restrict__ in, v4u* _
     }
 }
 
+// WG w copies rows [w*R, w*R+R) in order (ROT = 0) or starting at a per-WG
+// phase and wrapping inside its piece (ROT = 1): with long pieces and every
+// WG in lock step, rows w*R + s of all WGs share their low address bits
+template <int PF, bool ROT>
+__global__ __launch_bounds__(256) void k_rows_rot(const v4u* __restrict__ a, v4u* __restrict__ b, int R, int nrows)
+{
+    const int r0 = blockIdx.x * R;
+    const int t = threadIdx.x;
+    const int phase = ROT ? (int)((blockIdx.x * 2654435761u) >> 7) % R : 0;
+    for (int s = 0; s < R; s += PF) {
+        v4u v[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            int rr = s + u + phase;
+            rr = rr >= R ? rr - R : rr;
+            v[u] = a[(size_t)(r0 + rr) * 256 + t];
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            int rr = s + u + phase;
+            rr = rr >= R ? rr - R : rr;
+            __builtin_nontemporal_store(v[u], &b[(size_t)(r0 + rr) * 256 + t]);
+        }
+    }
+}
+
 int main()
 {
     const int W = 2048, H = 2048, Z = 64;
@@ -195,6 +221,16 @@ int main()
             hipLaunchKernelGGL((k_rows<8, true>), dim3(nrows / 16), dim3(256), 0, 0, (const v4u*)a, (v4u*)b, 16,
                                nrows);
         });
+        for (int R : {128, 512})
+            for (int rot = 0; rot < 2; ++rot)
+                run("rows_R" + std::to_string(R) + (rot ? "_rot" : "_seq"), cp, [&] {
+                    if (rot)
+                        hipLaunchKernelGGL((k_rows_rot<4, true>), dim3(nrows / R), dim3(256), 0, 0, (const v4u*)a,
+                                           (v4u*)b, R, nrows);
+                    else
+                        hipLaunchKernelGGL((k_rows_rot<4, false>), dim3(nrows / R), dim3(256), 0, 0, (const v4u*)a,
+                                           (v4u*)b, R, nrows);
+                });
         run("strip512_rpp512", cp, [&] {
             hipLaunchKernelGGL((k_strip<512, 4>), dim3(Z * 4 * 4), dim3(256), 0, 0, a, b, W, H, Z, 512);
         });

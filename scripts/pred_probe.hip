@@ -1,0 +1,153 @@
+// pred_probe.hip -- shape sweep of the vectorised predictor kernel (not part
+// of the product): includes csrc/lfm_predict.hip and times predict_vec over
+// the config-3 stack (2048 x 2048 x 64 uint16, angle family, Nnum 15) for
+// several (strip width, compute waves, rows per wave, prefetch) shapes, each
+// as the real predictor (K = 4) and as a copy through the same ring (K = 0),
+// next to the round-2 kernel (predict_ring) and a plain 8-row copy; checks
+// the vec output against predict_ring's bit for bit.
+//   hipcc --offload-arch=gfx950 -O3 -I include/lfm -I lightfieldmicroscopy_pc-bzip2_amd/csrc \
+//         scripts/pred_probe.hip -o exp/pred_probe
+#include "../lightfieldmicroscopy_pc-bzip2_amd/csrc/lfm_predict.hip"
+#include <cstdio>
+#include <string>
+
+extern "C" int lfm_hip_force_generic(void) { return 0; }
+
+using namespace lfm;
+
+__global__ void fill_kernel(uint16_t* p, size_t n, uint32_t seed)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 13;
+        h *= 0x5bd1e995u;
+        h ^= h >> 15;
+        const uint32_t x = (uint32_t)(i % 2048), y = (uint32_t)((i / 2048) % 2048);
+        p[i] = (uint16_t)(1000 + ((x * 7 + y * 3) & 1023) + (h & 63));
+    }
+}
+
+__global__ void cmp_kernel(const uint16_t* a, const uint16_t* b, size_t n, unsigned long long* bad)
+{
+    unsigned long long c = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c += a[i] != b[i];
+    if (c) atomicAdd(bad, c);
+}
+
+static hipEvent_t e0, e1;
+
+template <class F>
+static float time_it(F launch, int it = 20)
+{
+    launch();
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < it; ++i) launch();
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / it;
+}
+
+template <int PF>
+__global__ __launch_bounds__(256) void k_rows_nt(const v4u* __restrict__ a, v4u* __restrict__ b, int R, int nrows)
+{
+    const int r0 = blockIdx.x * R;
+    const int r1 = min(nrows, r0 + R);
+    const int t = threadIdx.x;
+    for (int r = r0; r < r1; r += PF) {
+        v4u v[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) v[u] = r + u < r1 ? a[(size_t)(r + u) * 256 + t] : v4u{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < PF; ++u)
+            if (r + u < r1) __builtin_nontemporal_store(v[u], &b[(size_t)(r + u) * 256 + t]);
+    }
+}
+
+int main(int argc, char** argv)
+{
+    const int W = 2048, H = 2048, Z = 64, T = 15;
+    const size_t n = (size_t)W * H * Z, bytes = n * 2;
+    const double alg = 2.0 * bytes;
+    uint16_t *in = nullptr, *ref = nullptr, *out = nullptr;
+    unsigned long long* bad = nullptr;
+    if (hipMalloc(&in, bytes) || hipMalloc(&ref, bytes) || hipMalloc(&out, bytes) || hipMalloc(&bad, 8)) return 1;
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, in, n, 12345u);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    FrameSet p{in, nullptr, ref, W, H, T, Z, 0, 0, 0};
+    auto report = [&](const std::string& name, float ms, long long mism) {
+        printf("{\"probe\": \"%s\", \"ms\": %.4f, \"TBps\": %.3f, \"frac_8TBs\": %.4f, \"mismatch\": %lld}\n",
+               name.c_str(), ms, alg / ms / 1e9, alg / ms / 1e9 / 8.0, mism);
+        fflush(stdout);
+    };
+    auto check = [&]() -> long long {
+        (void)hipMemset(bad, 0, 8);
+        hipLaunchKernelGGL(cmp_kernel, dim3(4096), dim3(256), 0, 0, out, ref, n, bad);
+        unsigned long long h = 0;
+        (void)hipMemcpy(&h, bad, 8, hipMemcpyDeviceToHost);
+        return (long long)h;
+    };
+    const int reps = argc > 1 ? std::atoi(argv[1]) : 2;
+    for (int rep = 0; rep < reps; ++rep) {
+        report("rows_R8_pf4_ntst_copy", time_it([&] {
+                   hipLaunchKernelGGL((k_rows_nt<4>), dim3(H * Z / 8), dim3(256), 0, 0, (const v4u*)in, (v4u*)out, 8,
+                                      H * Z);
+               }), -1);
+        // round-2 kernel per family (its output is the reference for the parity checks)
+#define REF(FAM, NAME, RPW, PD)                                                                                    \
+    {                                                                                                              \
+        const void* fn = (const void*)predict_ring<FAM, 4, 4, RPW, PD>;                                            \
+        Plan pl;                                                                                                   \
+        p.out = ref;                                                                                               \
+        (void)make_plan(p, fn, 4, RPW, PD, 1, pl);                                                                 \
+        report(std::string("ring_round2_") + NAME + "P4", time_it([&] { (void)launch_plan(fn, p, pl, 4, 1, 0); }), -1); \
+    }
+#define SHAPE(FAM, NAME, WPR, NCW, RPW, PD)                                                                        \
+    {                                                                                                              \
+        p.out = out;                                                                                               \
+        const std::string nm = "vec_w" #WPR "_c" #NCW "_r" #RPW "_pd" #PD;                                         \
+        (void)hipMemset(out, 0, bytes);                                                                            \
+        const float ms4 = time_it([&] { (void)launch_vec_shape<FAM, 4, 15, WPR, NCW, RPW, PD>(p, 0); });           \
+        report(nm + "_" + NAME + "P4", ms4, check());                                                              \
+    }
+#define SHAPES(FAM, NAME)                                                                                          \
+    SHAPE(FAM, NAME, 1, 4, 1, 3)                                                                                   \
+    SHAPE(FAM, NAME, 1, 4, 2, 2)                                                                                   \
+    SHAPE(FAM, NAME, 2, 8, 1, 3)                                                                                   \
+    SHAPE(FAM, NAME, 4, 8, 2, 4)                                                                                   \
+    SHAPE(FAM, NAME, 4, 12, 1, 4)                                                                                  \
+    SHAPE(FAM, NAME, 4, 12, 1, 5)
+        REF(1, "angle", 1, 3)
+        SHAPES(1, "angle")
+        REF(0, "tiles", 2, 2)
+        SHAPES(0, "tiles")
+        REF(2, "space", 1, 3)
+        SHAPES(2, "space")
+#define COPY(WPR, NCW, RPW, PD)                                                                                    \
+    report("vec_w" #WPR "_c" #NCW "_r" #RPW "_pd" #PD "_copy",                                                     \
+           time_it([&] { (void)launch_vec_shape<1, 0, 15, WPR, NCW, RPW, PD>(p, 0); }), -1);
+        p.out = out;
+        COPY(1, 4, 1, 3)
+        COPY(4, 8, 2, 4)
+        COPY(4, 12, 1, 5)
+        {
+            const void* fn0 = (const void*)predict_ring<1, 0, 4, 1, 3>;
+            Plan pl;
+            (void)make_plan(p, fn0, 4, 1, 3, 1, pl);
+            report("ring_round2_copy", time_it([&] { (void)launch_plan(fn0, p, pl, 4, 1, 0); }), -1);
+        }
+#undef COPY
+#undef SHAPES
+#undef REF
+#undef SHAPE
+    }
+    (void)hipFree(in);
+    (void)hipFree(ref);
+    (void)hipFree(out);
+    (void)hipFree(bad);
+    return 0;
+}

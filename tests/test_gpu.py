@@ -595,6 +595,56 @@ def test_pipelined_submit_wait(lfmlib, oracle, gpu):
         lfmlib.set_family("tiles")
 
 
+def test_submit_releases_unpredicted_device_input(lfmlib, oracle, gpu):
+    """A submit whose stack skips the predictor stage (forced predictor 0,
+    request 8) returns with the caller's device image no longer referenced:
+    overwriting the tensor before wait() must not change the .lfm."""
+    torch = gpu
+    stack = oracle.synthetic_lf(480, 400, Z=16, T=15, seed=77)[0, 0]
+    exp = oracle.encode(stack, header_version=8, nnum=15, family="tiles")
+    enc = lfmlib.Encoder(device=0)
+    try:
+        d = dev16(torch, stack)
+        t = enc.submit(d, header_version=8, nnum=15)
+        d.fill_(0x1234)  # a camera ring buffer refilling the slot
+        torch.cuda.synchronize()
+        b, st = enc.wait(t)
+        assert b == exp and st["chosen"] == 0
+    finally:
+        enc.close()
+
+
+def test_submit_select_frame_and_wait_codes(lfmlib, oracle, gpu):
+    """Auto-selection inside submit on a slab: select_frame = the whole
+    stack's frame 0 makes every slab select what the whole stack selects
+    (bytes equal the forced-slab encode); an auto slab without it is refused;
+    waiting on a ticket never issued returns code 8 and no buffer."""
+    import ctypes
+    torch = gpu
+    stack = oracle.synthetic_lf(480, 400, Z=24, T=15, seed=5150)[0, 0]
+    lfmlib.set_family("angle")
+    try:
+        k, _ = oracle.select(stack[0], 15, "angle")
+        exp = oracle.encode(stack[8:], header_version=8 + k, nnum=15, family="angle", z0=8)
+        enc = lfmlib.Encoder(device=0)
+        d = dev16(torch, stack)
+        t = enc.submit(d[8:], z0=8, header_version=0, nnum=15, select_frame=d[0])
+        b, st = enc.wait(t)
+        assert b == exp and st["chosen"] == k and st["select_ms"] > 0
+        # the same from host memory
+        t = enc.submit(stack[8:], z0=8, header_version=0, nnum=15, select_frame=stack[0])
+        assert enc.wait(t)[0] == exp
+        with pytest.raises(lfmlib.LfmError):
+            enc.submit(d[8:], z0=8, header_version=0, nnum=15)
+        out = ctypes.POINTER(ctypes.c_uint8)()
+        n = ctypes.c_uint64(123)
+        rc = lfmlib.lib().lfm_encoder_wait(enc._h, 987654321, ctypes.byref(out), ctypes.byref(n), None)
+        assert rc == 8 and not out and n.value == 0
+        enc.close()
+    finally:
+        lfmlib.set_family("tiles")
+
+
 @pytest.mark.parametrize("env", ["LFM_DECODE_H2D=1", "LFM_DECODE_H2D=2",
                                  "LFM_WALK_LDSM=0 LFM_WALK_THREADS=256", "LFM_WALK_THREADS=1024 LFM_TT_THREADS=1024"])
 def test_decode_path_switches(lfmlib, oracle, gpu, tmp_path, env):
