@@ -524,6 +524,23 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     const int p = par_;
     Inflight& f = fly_[p];
     if (f.th.joinable()) f.th.join();  // the encode before last used this buffer set
+    // Auto-selection (klb_imageIO.cpp:2316-2360) runs FIRST, before waiting for
+    // the previous encode's release: its short kernels interleave with that
+    // encode's GPU bzip2 instead of adding to this encode's critical path.  The
+    // request then becomes the forced 8 + k (video bit kept) for the predictor
+    // stage; the bytes are the same.
+    const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
+    const int req0 = h.headerVersion & 0x7F;
+    int pre_k = -1;
+    float pre_ent[8] = {0};
+    double pre_ms = 0.0;
+    if (gpu_bz && req0 < NUM_PREDICTORS && h.getBytesPerPixel() == 2 && h.Nnum > 0) {
+        auto ts0 = clk::now();
+        if (int rc = preselect(img, dev, h, slab ? *slab : whole, &pre_k, pre_ent)) return rc;
+        pre_ms = ms_since(ts0);
+        h.headerVersion = (uint8_t)((h.headerVersion & 0x80) | (8 + pre_k));
+        if (trace) ts("selected");
+    }
     fly_[p ^ 1].wait_release();        // the previous encode is in its tail
     if (trace) ts("released");
     f.ticket = next_ticket_++;
@@ -537,6 +554,10 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     }
     if (ticket) *ticket = f.ticket;
     par_ ^= 1;
+    if (pre_k >= 0) {
+        f.st.select_ms = pre_ms;
+        std::memcpy(f.st.entropy, pre_ent, sizeof(pre_ent));
+    }
     auto t0 = clk::now();
     int level = slab ? slab->level : -1;
     if (level < 1 && slab && slab->z0 > 0 && h.getBytesPerPixel()) {
@@ -546,7 +567,6 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         if (nominal.blockSize[2] == 0) nominal.blockSize[2] = 1;
         level = bzip2_level(nominal);
     }
-    const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
     if (!gpu_bz) {  // no GPU bzip2: the whole encode here
         MemSink sink(&mem_ring[p]);
         f.rc = encode_set(img, dev, h, sink, &f.st, threads, slab, p);
@@ -615,14 +635,16 @@ int Encoder::ensure_gpu()
         if (hipGetDevice(&device_) != hipSuccess) device_ = 0;
     }
     if (device_ >= n || hipSetDevice(device_) != hipSuccess) return kErrNoGpu;
-    // the predictor stage (selection + fused predictor) runs at the device's
-    // highest stream priority: a pipelined submit's short kernels then go ahead
+    // the predictor stage (selection + fused predictor) can run at the device's
+    // highest stream priority, so a pipelined submit's short kernels go ahead
     // of the previous encode's GPU bzip2 work still queued on the other streams
+    // (env LFM_PRED_PRIO=1; off by default: measured slower end to end)
+    static const bool prio = std::getenv("LFM_PRED_PRIO") && std::atoi(std::getenv("LFM_PRED_PRIO")) == 1;
     int prio_lo = 0, prio_hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
-    if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_hi) != hipSuccess &&
-        hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess)
-        return kErrNoGpu;
+    if (!prio || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
+    }
     (void)hipEventCreate(&ev0_);
     (void)hipEventCreate(&ev1_);
     gpu_ready_ = true;
@@ -1075,6 +1097,24 @@ int normalize_header(klb_image_header& h)
         return 5;
     }
     return 0;
+}
+
+// selection for submit: on the slab's select_frame, else on frame 0 of the image
+int Encoder::preselect(const void* img, bool dev, const klb_image_header& h, const SlabSpec& slab, int* k,
+                       float ent[8])
+{
+    if (int rc = ensure_gpu()) return rc;
+    (void)hipSetDevice(device_);
+    const int W = (int)h.xyzct[0], H = (int)h.xyzct[1];
+    if (W <= 0 || H <= 0) return 3;
+    const void* frame = slab.select_frame ? slab.select_frame : (slab.z0 > 0 ? nullptr : img);
+    if (!frame) return 3;  // a slab's own frame 0 is not the stack's
+    if (!dev) return select_host_frame(frame, W, H, h.Nnum, current_family(), k, ent);
+    if (!dev_alloc(d_ws_, d_ws_cap_, lfm_hip_select_workspace_bytes(W, H))) return 3;
+    return lfm_hip_select((const uint16_t*)frame, W, H, h.Nnum, current_family(), ent, k, d_ws_, stream_) ==
+                   LFM_HIP_OK
+               ? 0
+               : 3;
 }
 
 int Encoder::select_host_frame(const void* frame, int W, int H, int T, int family, int* chosen, float entropy[8])

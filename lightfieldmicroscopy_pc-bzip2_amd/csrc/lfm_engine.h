@@ -176,6 +176,7 @@ private:
                      Inflight* fly);
     int encode_set(const void* img, bool dev, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int threads,
                    const SlabSpec* slab, int set);
+    int preselect(const void* img, bool dev, const klb_image_header& h, const SlabSpec& slab, int* k, float ent[8]);
     int ensure_gpu();
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     void join_inflight();
