@@ -28,6 +28,13 @@ N > 1 (`verified` in the JSON line).  At N = 1 the same stack is also encoded
 from host memory (pinned and pageable), H2D inside the timed region:
 `host_input` (the PCIe-inclusive rate; `value` is always HBM-resident).
 
+At N = 1 two more legs follow (not the metric): `config5` -- four full
+t-volumes of config 5 (4096 x 4096 x 32 x 1 x 4, video, tiles) encoded from
+HBM into one .lfm (SHA-256 checked) and decoded back, the per-GPU rate of the
+config-5 round trip; `inproc` -- the drop-in multi-GPU writer
+(lfm_encoder_encode_multi, what klb_imageIO::writeImage / writeKLBstack run)
+on config 4 from host memory, on this device and on every visible device.
+
 Also reported: `roofline` of the dominant kernel (fused predictor, HIP-event
 time per launch on its own stream) and `cpu_baseline` = the reference's CPU
 bzip2-only path (request 8, same blocks, the reference's own bzip2-1.0.6 from
@@ -150,12 +157,30 @@ def verify_lfm(buf, world, zf):
                        % (nlay, len(e["layer_sha256"]) * 8), "ok": bool(ok)}
 
 
+def _free_bytes(d):
+    try:
+        st = os.statvfs(d)
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return 0
+
+
 class SharedLfm:
-    """The whole stack's .lfm in host shared memory, written by every rank."""
+    """The whole stack's .lfm in host shared memory, written by every rank.
+    The file is sparse: writes beyond the filesystem's free space would fault
+    (SIGBUS on the mapping), so /dev/shm is used only when it can hold the
+    whole capacity, else /tmp (same check), else the run stops with a message."""
 
     def __init__(self, rank, world, cap):
         port = os.environ.get("MASTER_PORT", "0")
-        d = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+        need = int(cap * 1.02) + (64 << 20)
+        d = None
+        for cand in ("/dev/shm", os.environ.get("TMPDIR", "/tmp"), "/tmp"):
+            if os.path.isdir(cand) and _free_bytes(cand) >= need:
+                d = cand
+                break
+        if d is None:
+            raise RuntimeError("no filesystem for the shared .lfm: need %.2f GB free in /dev/shm or /tmp" % (need / 1e9))
         self.path = os.path.join(d, "lfm_bench_%s_%d_%d.lfm" % (port, world, os.getuid()))
         self.rank = rank
         if rank == 0:
@@ -211,6 +236,105 @@ def host_input_rates(enc, d_img, zf, steps=2):
     return out
 
 
+def config5_leg(local, threads, nvol=4):
+    """Config 5 at full frame size on this GPU: nvol t-volumes of the 4096 x
+    4096 x 32 video stack (tiles, Nnum 13, auto-selected on volume 0's frame
+    0), resident in HBM, encoded into ONE .lfm (predictor per volume + GPU
+    bzip2 + D2H), SHA-256 checked against the oracle (cfg5x4); then decoded
+    (GPU bzip2 decode + GPU inverse predictor + D2H into a fresh host array)
+    and compared with the input.  SURVEY 8(d) config 5 is the 100-volume
+    encode + decode round trip; every volume codes alone, so this is its
+    per-GPU rate."""
+    X5, Y5, Z5, T5, seed = 4096, 4096, 32, 13, 0x4C464D05
+    e = _manifest("cfg5x4_4096x4096x32x1x4_video_tiles_auto")
+    d = torch.empty((nvol, 1, Z5, Y5, X5), dtype=torch.int16, device="cuda")
+    for t in range(nvol):
+        lfm.synth_device(d[t, 0], X5, Y5, Z5, T5, t_index=t, idx0=t * Z5 * X5 * Y5, seed=seed)
+    torch.cuda.synchronize()
+    lfm.set_family("tiles")
+    px = nvol * X5 * Y5 * Z5
+    enc = lfm.Encoder(device=local, num_threads=threads)
+    try:
+        enc.encode(d, header_version=0x80, nnum=T5, copy=False)  # warm: buffers sized and first-touched
+        runs = []
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            b, st = enc.encode(d, header_version=0x80, nnum=T5, copy=False)
+            runs.append((time.perf_counter() - t0) * 1e3)
+        buf = bytes(b)
+    finally:
+        enc.close()
+    ok = None
+    if e is not None and nvol == e["xyzct"][4]:
+        ok = hashlib.sha256(buf).hexdigest() == e["sha256"] and len(buf) == e["size"]
+    ref = d.cpu().numpy().view(np.uint16)
+    del d
+    dl = []
+    exact = True
+    for _ in range(2):
+        t0 = time.perf_counter()
+        img = lfm.decode(buf, num_threads=threads)
+        dl.append((time.perf_counter() - t0) * 1e3)
+        exact = exact and bool(np.array_equal(img.reshape(ref.shape), ref))
+        del img
+    lfm.set_family(FAMILY)
+    ems, dms = min(runs), dl[-1]
+    return {"workload": "%d t-volumes of config 5 (4096x4096x32x1x%d, video bit, tiles, Nnum 13, auto), one .lfm"
+                        % (nvol, nvol),
+            "encode_Mpixel_per_s": round(px / ems / 1e3, 1), "encode_ms": round(ems, 2),
+            "encode_runs_ms": [round(x, 2) for x in runs], "chosen_predictor": st["chosen"],
+            "ratio": round(px * 2 / len(buf), 4),
+            "verified": {"against": "cfg5x4 whole-file SHA-256 (oracle, reference bzip2-1.0.6)", "ok": ok},
+            "decode_Mpixel_per_s": round(px / dms / 1e3, 1), "decode_ms": round(dms, 1),
+            "decode_runs_ms": [round(x, 1) for x in dl], "decode_exact": exact,
+            "round_trip_Mpixel_per_s": round(px / (ems + dms) / 1e3, 1),
+            "note": "encode from HBM to the in-memory .lfm; decode from the in-memory .lfm to a host array (PCIe "
+                    "upload of the payload and download of the pixels included)"}
+
+
+def inproc_leg(local, threads, ndevs):
+    """The drop-in multi-GPU writer -- lfm_encoder_encode_multi, the block
+    scheduler behind klb_imageIO::writeImage / writeKLBstack -- on config 4
+    (2048 x 2048 x 256 uint16, tiles, Nnum 15, auto) from HOST memory: z-slabs
+    of whole block layers farmed to each device list in ndevs, one host thread
+    per device, in-order writer; PCIe-inclusive; SHA-256 checked (cfg4)."""
+    X4, Y4, Z4, T4, seed = 2048, 2048, 256, 15, 0x4C464D04
+    e = _manifest("cfg4_2048x2048x256_tiles_auto")
+    d = torch.empty((Z4, Y4, X4), dtype=torch.int16, device="cuda")
+    lfm.synth_device(d, X4, Y4, Z4, T4, seed=seed)
+    host = torch.empty((Z4, Y4, X4), dtype=torch.int16, pin_memory=True)
+    host.copy_(d)
+    del d
+    arr = host.numpy().view(np.uint16)
+    lfm.set_family("tiles")
+    out = {"workload": "config 4: 2048x2048x256 uint16 from host memory, tiles, Nnum 15, auto, 96x96x8 blocks",
+           "path": "lfm_encoder_encode_multi (klb_imageIO::writeImage's scheduler): z-slabs per device, in-order "
+                   "writer, H2D inside the timed region"}
+    px = X4 * Y4 * Z4
+    enc = lfm.Encoder(device=local, num_threads=threads)
+    try:
+        for devs in ndevs:
+            lfm.set_devices(devs)
+            b, _ = enc.encode_multi(arr, header_version=0, nnum=T4, copy=False)  # warm (per-device encoders)
+            runs = []
+            for _ in range(2):
+                t0 = time.perf_counter()
+                b, st = enc.encode_multi(arr, header_version=0, nnum=T4, copy=False)
+                runs.append((time.perf_counter() - t0) * 1e3)
+            ok = None if e is None else (len(b) == e["size"] and hashlib.sha256(b).hexdigest() == e["sha256"])
+            ms = min(runs)
+            out["gpus_%d" % len(devs)] = {"devices": devs, "Mpixel_per_s": round(px / ms / 1e3, 1),
+                                          "ms": round(ms, 2), "runs_ms": [round(x, 2) for x in runs],
+                                          "verified": ok}
+    finally:
+        lfm.set_devices([])
+        enc.close()
+        lfm.release_encoders()
+        lfm.set_family(FAMILY)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +344,8 @@ def main():
     ap.add_argument("--frames", type=int, default=Z)
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-host-input", action="store_true")
+    ap.add_argument("--no-config5", action="store_true")
+    ap.add_argument("--no-inproc", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -393,6 +519,12 @@ def main():
                           "first_ms": round(dlist[0], 1), "runs_ms": [round(x, 1) for x in dlist],
                           "exact": exact,
                           "path": "GPU bzip2 decode + GPU inverse predictor (host libbz2 only for flagged streams, %d threads)" % threads}
+    if rank == 0 and world == 1 and not args.no_config5:
+        line["config5"] = config5_leg(local, threads)
+    if rank == 0 and world == 1 and not args.no_inproc:
+        nvis = torch.cuda.device_count()
+        legs = [[local]] + ([list(range(nvis))] if nvis > 1 else [])
+        line["inproc"] = inproc_leg(local, threads, legs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)
         line["cpu_baseline"]["affinity_cpus"] = len(os.sched_getaffinity(0))

@@ -409,10 +409,14 @@ __device__ __forceinline__ void band3(const UnFrames& p, int fz, uint16_t* ring,
 constexpr int kHand = 128;
 constexpr int kSync = 32;
 
-template <int FAM, int K, bool TEMP>
+// XCU (cross-CU, band5 below): every band is its own workgroup, so `pos` lives
+// in global memory and the progress words, their fences and the hand-over
+// loads of the band above's rows use agent scope instead of workgroup scope.
+template <int FAM, int K, bool TEMP, bool XCU = false>
 __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv, uint16_t* lds, int ring_off,
                                       int hand_off, int* pos)
 {
+    constexpr int kScope = XCU ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP;
     const int r = threadIdx.x & 63;
     const size_t fs = (size_t)p.W * p.H;
     const uint16_t* sym = p.sym + fz * fs;
@@ -424,18 +428,20 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
     // (bounded: a broken hand-over shows up as wrong pixels, never as a hang)
     auto wait_ge = [&](int need) {
         for (int spin = 0; spin < (1 << 24) &&
-                           __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED,
-                                                                            __HIP_MEMORY_SCOPE_WORKGROUP)) < need;
+                           __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope)) <
+                               need;
              ++spin)
             __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if constexpr (XCU) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
     // the band's stores are complete (in the CU's write-through L1 / the L2)
     // before its progress is published
     auto publish = [&](int v) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if constexpr (XCU) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_s_waitcnt(0);
-        if (r == 0) __hip_atomic_store(pos + wv, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (r == 0) __hip_atomic_store(pos + wv, v, __ATOMIC_RELAXED, kScope);
     };
     auto far = [&](int x, int dx, int dy) -> int {
         const int rr = r + dy;
@@ -461,7 +467,7 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int c = min(c0 + hc + 2 * q, W - 2);
-                hv[q] = __hip_atomic_load(hsrc + (c >> 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                hv[q] = __hip_atomic_load(hsrc + (c >> 1), __ATOMIC_RELAXED, kScope);
             }
         };
         auto hstore = [&](int c0) {
@@ -590,6 +596,24 @@ __global__ __launch_bounds__(512) void unpredict_band4(UnFrames p, int NW)
     else band4<FAM, K, false>(p, fz, NW, wv, lds4, ring_off, hand_off, pos);
 }
 
+// band5: the band pipeline spread over the whole chip -- one single-wave
+// workgroup per (band, frame), blockIdx = band * nfr + frame, so every band is
+// dispatched after the band above it (the one it waits for) and, with nfr a
+// multiple of 8, all bands of a frame share an XCD (one L2).  Progress words
+// (one per band, -1 before the launch) live in global memory.  Config 3: 2048
+// waves over 256 CUs instead of 64 workgroups of 8 waves on 64 CUs.
+template <int FAM, int K>
+__global__ __launch_bounds__(64) void unpredict_band5(UnFrames p, int* pos_all, int nbands, int nfr)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds5[];
+    const int b = (int)blockIdx.x / nfr, fi = (int)blockIdx.x - b * nfr;
+    const int fz = p.first + fi * p.step;
+    if (fz >= p.nz || b >= nbands) return;
+    int* pos = pos_all + (size_t)fi * nbands;
+    if (p.video && ((p.z0 + fz) & 1)) band4<FAM, K, true, true>(p, fz, nbands, b, lds5, 0, 64 * kRing, pos);
+    else band4<FAM, K, false, true>(p, fz, nbands, b, lds5, 0, 64 * kRing, pos);
+}
+
 template <int FAM, int K>
 __global__ __launch_bounds__(64) void unpredict_band3(UnFrames p)
 {
@@ -636,9 +660,34 @@ static int band4_waves(const UnFrames& p)
     return nw >= 2 ? nw : 0;
 }
 
+// band5 unless LFM_UNPREDICT_XCU=0 (band4 then keeps a frame's bands on one CU)
+static bool band5_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("LFM_UNPREDICT_XCU");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 template <int FAM, int K_>
 static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
 {
+    if (band4_waves(p) && band5_enabled()) {
+        const int nbands = (p.H + 63) / 64;
+        const size_t lds = (size_t)(64 * kRing + (p.T + 1) * kHand) * 2;
+        int* pos = nullptr;
+        const size_t pbytes = (size_t)grid * nbands * sizeof(int);
+        if (hipMallocAsync((void**)&pos, pbytes, st) != hipSuccess) return hipErrorOutOfMemory;
+        hipError_t e = hipMemsetAsync(pos, 0xFF, pbytes, st);  // -1: no progress yet
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL((unpredict_band5<FAM, K_>), dim3(grid * nbands), dim3(64), lds, st, p, pos, nbands,
+                               grid);
+            e = hipGetLastError();
+        }
+        (void)hipFreeAsync(pos, st);
+        return e;
+    }
     if (const int nw = band4_waves(p)) {
         const size_t lds = (size_t)nw * (64 * kRing + (p.T + 1) * kHand) * 2;
         const void* fn4 = (const void*)unpredict_band4<FAM, K_>;

@@ -322,16 +322,20 @@ def splitmix64(x):
     return z ^ (z >> 31)
 
 
-def synthetic_lf(X, Y, Z=1, C=1, Tn=1, T=15, seed=0x4C464D00, z0=0):
+def synthetic_lf(X, Y, Z=1, C=1, Tn=1, T=15, seed=0x4C464D00, z0=0, t0=0, idx0=None):
     """SURVEY.md section 8(d) integer light-field generator (numpy restatement).
     z0 > 0 (C = Tn = 1): frames [z0, z0 + Z) of a taller stack, so large
-    stacks can be generated slab by slab."""
-    if z0:
+    stacks can be generated slab by slab.  t0 / idx0 (C = Tn = 1): frames of
+    t-volume t0 of a larger 5-D stack whose linear index starts at idx0 (for
+    frames z0.. of volume t0 of an X x Y x Zv x 1 x Tn stack:
+    idx0 = (t0 * Zv + z0) * X * Y), so multi-volume stacks can be generated
+    one volume (or slab) at a time."""
+    if z0 or t0 or idx0 is not None:
         assert C == 1 and Tn == 1
     x = np.arange(X, dtype=np.int64)[None, None, None, None, :]
     y = np.arange(Y, dtype=np.int64)[None, None, None, :, None]
     z = np.arange(z0, z0 + Z, dtype=np.int64)[None, None, :, None, None]
-    t = np.arange(Tn, dtype=np.int64)[:, None, None, None, None]
+    t = np.arange(t0, t0 + Tn, dtype=np.int64)[:, None, None, None, None]
     du = (x % T) - T // 2
     dv = (y % T) - T // 2
     r2 = du * du + dv * dv
@@ -342,7 +346,8 @@ def synthetic_lf(X, Y, Z=1, C=1, Tn=1, T=15, seed=0x4C464D00, z0=0):
         return np.abs((a % 2048) - 1024)
     field = 256 + tri(3 * x + 40 * z + 97 * t) // 4 + tri(2 * y) // 4
     shape = (Tn, C, Z, Y, X)
-    idx = np.arange(z0 * Y * X, z0 * Y * X + int(np.prod(shape)), dtype=np.uint64).reshape(shape)
+    i0 = z0 * Y * X if idx0 is None else int(idx0)
+    idx = np.arange(i0, i0 + int(np.prod(shape)), dtype=np.uint64).reshape(shape)
     noise = (_splitmix_vec(np.uint64(seed) ^ (idx * np.uint64(0x9E3779B97F4A7C15))) >> np.uint64(58)).astype(np.int64)
     v = 100 + (lens * field) // 256 + noise
     return np.broadcast_to(v, shape).astype(np.uint16)

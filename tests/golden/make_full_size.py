@@ -44,11 +44,16 @@ CONFIGS = {
     # config 5: one t-volume (t = 0) of the 4096 x 4096 x 32 x 1 x 100 video stack;
     # blocks never span t, so every t-volume is coded alone
     "cfg5v0_4096x4096x32_video_tiles_auto": (4096, 4096, 32, 13, "tiles", 0x80, 0x4C464D05),
+    # config 5, four t-volumes (t = 0..3) of the same stack: one .lfm of the
+    # 4096 x 4096 x 32 x 1 x 4 video stack; selection on frame 0 of volume 0,
+    # every volume's z loop coded alone;
+    # volume_sha256[t] = SHA-256 of volume t's block streams
+    "cfg5x4_4096x4096x32x1x4_video_tiles_auto": (4096, 4096, 32, 13, "tiles", 0x80, 0x4C464D05, 4),
 }
 BLOCK = [96, 96, 8, 1, 1]  # default uint16 block (klb_imageHeader.cpp:301-309)
 
 
-def encode_full(X, Y, Z, T, family, hv, seed, threads):
+def encode_full(X, Y, Z, T, family, hv, seed, threads, Tn=1):
     bz = O.bzip2()
     assert "reference" in bz.kind, "build oracle/_ref first (make -C oracle)"
     video = hv >> 7
@@ -59,33 +64,39 @@ def encode_full(X, Y, Z, T, family, hv, seed, threads):
     else:
         k, ent = req - 8, None
     hv_out = (hv & 0x80) | k
-    bs = [min(b, x) for b, x in zip(BLOCK, [X, Y, Z, 1, 1])]
+    bs = [min(b, x) for b, x in zip(BLOCK, [X, Y, Z, 1, Tn])]
     level = min(9, -(-2 * int(np.prod(bs)) // 100000))
     nbx, nby = math.ceil(X / bs[0]), math.ceil(Y / bs[1])
     blobs = []
     layers = []
-    prev_raw = None
+    volumes = []
     with ThreadPoolExecutor(threads) as ex:
-        for z0 in range(0, Z, bs[2]):
-            dz = min(bs[2], Z - z0)
-            raw = O.synthetic_lf(X, Y, Z=dz, T=T, seed=seed, z0=z0)[0, 0]
-            sym = np.empty_like(raw)
-            for j in range(dz):
-                z = z0 + j
-                zf = (video & z) & 1
-                p = raw[j - 1] if j else prev_raw
-                sym[j] = O.predict_frame(raw[j], p if zf else None, T, family, k, zf) if k else raw[j]
-            prev_raw = raw[-1].copy()
+        for t in range(Tn):
+            prev_raw = None
+            vol = []
+            for z0 in range(0, Z, bs[2]):
+                dz = min(bs[2], Z - z0)
+                raw = O.synthetic_lf(X, Y, Z=dz, T=T, seed=seed, z0=z0, t0=t,
+                                     idx0=(t * Z + z0) * X * Y)[0, 0]
+                sym = np.empty_like(raw)
+                for j in range(dz):
+                    z = z0 + j
+                    zf = (video & z) & 1
+                    p = raw[j - 1] if j else prev_raw
+                    sym[j] = O.predict_frame(raw[j], p if zf else None, T, family, k, zf) if k else raw[j]
+                prev_raw = raw[-1].copy()
 
-            def one(b):
-                by, bx = divmod(b, nbx)
-                blk = np.ascontiguousarray(sym[:, by * bs[1]:(by + 1) * bs[1], bx * bs[0]:(bx + 1) * bs[0]])
-                return bz.compress(blk.tobytes(), level)
-            lay = list(ex.map(one, range(nbx * nby)))
-            layers.append(hashlib.sha256(b"".join(lay)).hexdigest())
-            blobs.extend(lay)
+                def one(b):
+                    by, bx = divmod(b, nbx)
+                    blk = np.ascontiguousarray(sym[:, by * bs[1]:(by + 1) * bs[1], bx * bs[0]:(bx + 1) * bs[0]])
+                    return bz.compress(blk.tobytes(), level)
+                lay = list(ex.map(one, range(nbx * nby)))
+                layers.append(hashlib.sha256(b"".join(lay)).hexdigest())
+                vol.extend(lay)
+            volumes.append(hashlib.sha256(b"".join(vol)).hexdigest())
+            blobs.extend(vol)
     offsets = np.cumsum([len(b) for b in blobs]).astype(np.uint64)
-    head = O.header_bytes(hv_out, T, [X, Y, Z, 1, 1], [1.0] * 5, 1, 1, None, bs, offsets)
+    head = O.header_bytes(hv_out, T, [X, Y, Z, 1, Tn], [1.0] * 5, 1, 1, None, bs, offsets)
     h = hashlib.sha256(head)
     for b in blobs:
         h.update(b)
@@ -93,7 +104,7 @@ def encode_full(X, Y, Z, T, family, hv, seed, threads):
     return dict(sha256=h.hexdigest(), size=size, final_header_version=hv_out, chosen=int(k),
                 entropy=None if ent is None else [float(e) for e in ent], layer_sha256=layers,
                 header_sha256=hashlib.sha256(head).hexdigest(), nblocks=len(blobs), level=level,
-                ratio=round(X * Y * Z * 2 / size, 4))
+                ratio=round(X * Y * Z * Tn * 2 / size, 4), **({"volume_sha256": volumes} if Tn > 1 else {}))
 
 
 def main():
@@ -103,14 +114,19 @@ def main():
     args = ap.parse_args()
     path = os.path.join(HERE, "full_size_manifest.json")
     man = {e["name"]: e for e in json.load(open(path))} if os.path.exists(path) else {}
-    for name, (X, Y, Z, T, fam, hv, seed) in CONFIGS.items():
+    for name, cfg in CONFIGS.items():
+        X, Y, Z, T, fam, hv, seed = cfg[:7]
+        Tn = cfg[7] if len(cfg) > 7 else 1
         if args.only and args.only != name:
             continue
         t0 = time.time()
-        r = encode_full(X, Y, Z, T, fam, hv, seed, args.threads)
-        e = dict(name=name, xyzct=[X, Y, Z, 1, 1], nnum=T, family=fam, header_version=hv, seed=seed,
-                 block_size=BLOCK, generator="synthetic_lf(%d,%d,%d,T=%d,seed=0x%X)" % (X, Y, Z, T, seed),
-                 bzip2=O.bzip2().kind, **r)
+        r = encode_full(X, Y, Z, T, fam, hv, seed, args.threads, Tn)
+        gen = "synthetic_lf(%d,%d,%d,T=%d,seed=0x%X)" % (X, Y, Z, T, seed)
+        if Tn > 1:
+            gen = "synthetic_lf(%d,%d,%d,Tn=%d,T=%d,seed=0x%X), one volume at a time (t0, idx0)" % (X, Y, Z, Tn, T,
+                                                                                                  seed)
+        e = dict(name=name, xyzct=[X, Y, Z, 1, Tn], nnum=T, family=fam, header_version=hv, seed=seed,
+                 block_size=BLOCK, generator=gen, bzip2=O.bzip2().kind, **r)
         man[name] = e
         print("%s: %d bytes, predictor %d, ratio %.3f, %.1f s" % (name, e["size"], e["chosen"], e["ratio"],
                                                                   time.time() - t0), flush=True)

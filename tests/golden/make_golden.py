@@ -115,6 +115,10 @@ def lfm_manifest(img_tif):
     g5 = O.synthetic_lf(128, 128, Z=8, C=1, Tn=3, T=13, seed=0x4C464D05)
     add("cfg5s_128x128x8x1x3_video_auto", g5, 0x80, 13, "tiles",
         gen="synthetic_lf(128,128,8,1,3,T=13,seed=0x4C464D05)")
+    # config 5 scaled as SURVEY 8(d) states it: 512 x 512 x 32 x 1 x 3 video, tiles, auto
+    g5b = O.synthetic_lf(512, 512, Z=32, C=1, Tn=3, T=13, seed=0x4C464D05)
+    add("cfg5s_512x512x32x1x3_video_auto", g5b, 0x80, 13, "tiles",
+        gen="synthetic_lf(512,512,32,1,3,T=13,seed=0x4C464D05)")
     small = O.synthetic_lf(70, 45, Z=3, T=13, seed=0x4C464D06)
     for fam in FAMS:
         for k in range(8):

@@ -155,6 +155,7 @@ def _gen(oracle, e):
 
 @pytest.mark.parametrize("name", ["cfg1_imgtif_page0_req8", "cfg1_imgtif_stack_req8", "cfg2_512x512_space_auto", "cfg3s_512x512x8_angle_auto",
                                   "cfg4s_256x256x16_tiles_auto", "cfg5s_128x128x8x1x3_video_auto",
+                                  "cfg5s_512x512x32x1x3_video_auto",
                                   "imgtif_page12_auto", "imgtif_stack_auto_video", "matlab_test_m"])
 def test_lfm_bytes_match_oracle_manifest(lfmlib, oracle, gpu, tmp_path, name):
     """Whole encode (GPU selection + predictor + host bzip2) gives the oracle's

@@ -106,3 +106,66 @@ def test_config5_volume_roundtrip(lfmlib, gpu):
         enc.close()
     out = lfmlib.decode(buf)
     assert np.array_equal(out.reshape(d.shape), d.cpu().numpy().view(np.uint16))
+
+
+_CFG5X4_CHILD = r"""
+import hashlib, json, os, sys, time
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import lfm
+e = json.loads(sys.argv[2])
+path = sys.argv[3]
+X, Y, Z, C, Tn = e["xyzct"]
+torch.cuda.set_device(0)
+d = torch.empty((Z, Y, X), dtype=torch.int16, device="cuda")
+img = np.empty((Tn, 1, Z, Y, X), dtype=np.uint16)
+for t in range(Tn):  # volume t of the stack: t term and linear index of the SURVEY 8(d) generator
+    lfm.synth_device(d, X, Y, Z, e["nnum"], t_index=t, idx0=t * Z * X * Y, seed=e["seed"])
+    img[t, 0] = d.cpu().numpy().view(np.uint16)
+del d
+lfm.set_family("tiles")
+t0 = time.perf_counter()
+lfm.write_lfm(path, img, predictor_request=0, nnum=e["nnum"], video=1)  # writeLFMstack_c -> writeImage
+t_enc = time.perf_counter() - t0
+buf = open(path, "rb").read()
+nb = e["nblocks"] // Tn
+offs = np.frombuffer(buf, dtype="<u8", count=e["nblocks"], offset=320)
+base, prev, vols = 320 + 8 * e["nblocks"], 0, []
+for t in range(Tn):
+    end = int(offs[(t + 1) * nb - 1])
+    vols.append(hashlib.sha256(buf[base + prev:base + end]).hexdigest())
+    prev = end
+t0 = time.perf_counter()
+back, hv, nn = lfm.read_lfm(path)  # readLFMstack_c -> readImageFull
+t_dec = time.perf_counter() - t0
+print(json.dumps({"sha256": hashlib.sha256(buf).hexdigest(), "size": len(buf), "volume_sha256": vols,
+                  "header_version": hv, "exact": bool(np.array_equal(back, img)),
+                  "encode_s": t_enc, "decode_s": t_dec, "devices": lfm.get_devices()}))
+"""
+
+
+@pytest.mark.timeout(600)
+def test_config5_four_volumes_t_sharded_writer(lfmlib, gpu, tmp_path):
+    """Config 5 at full frame size, four t-volumes (4096 x 4096 x 32 x 1 x 4,
+    video, tiles, auto) through the drop-in writer: writeLFMstack_c ->
+    klb_imageIO::writeImage farms the t-axis over LFM_GPUS=0,0,0,0 (four
+    workers on the test box's one GPU, lfm_multigpu.cpp) and the file equals
+    the oracle's (whole-file and per-volume SHA-256, full_size_manifest.json
+    cfg5x4); readLFMstack_c -> readImageFull returns every pixel.  Runs in a
+    child process (its own pooled encoders and workspace budget)."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    e = _full("cfg5x4_4096x4096x32x1x4_video_tiles_auto")
+    env = dict(os.environ, LFM_GPUS="0,0,0,0", LFM_BZ2_GPU_BUDGET_MB="6144")
+    r = subprocess.run([sys.executable, "-c", _CFG5X4_CHILD, PKG, json.dumps(e), str(tmp_path / "cfg5x4.lfm")],
+                       env=env, capture_output=True, text=True, timeout=560)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["devices"] == [0, 0, 0, 0]
+    assert got["volume_sha256"] == e["volume_sha256"]
+    assert got["sha256"] == e["sha256"] and got["size"] == e["size"]
+    assert got["header_version"] == e["final_header_version"]
+    assert got["exact"]
+    print("cfg5x4: encode %.2f s, decode %.2f s" % (got["encode_s"], got["decode_s"]))

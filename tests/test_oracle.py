@@ -231,3 +231,31 @@ def test_header_layout_fields(oracle):
     assert (hv, nnum) == (7, 13)
     h = oracle.parse_header(b)
     assert h["xyzct"] == [101, 151, 1, 1, 1] and h["nb"] == 1 and h["offsets"][-1] == len(b) - 328
+
+
+def test_config5_volume_parity_rule(oracle):
+    """blocks never span t, so the blocks of every
+    t-volume of a video stack equal that volume encoded alone with the
+    predictor forced to the one chosen on volume 0's frame 0 (request 8 + k),
+    and volume 0 alone with auto-selection gives the same bytes too.  Checked
+    on a 256 x 256 x 16 x 1 x 3 stack (the 512 x 512 x 32 x 1 x 3 digest is in
+    lfm_manifest.json, the 4096 x 4096 x 32 x 1 x 4 one in full_size_manifest.json)."""
+    X, Y, Z, Tn, T = 256, 256, 16, 3, 13
+    img = oracle.synthetic_lf(X, Y, Z=Z, C=1, Tn=Tn, T=T, seed=0x4C464D05)
+    whole = oracle.encode(img, header_version=0x80, nnum=T, family="tiles")
+    k = whole[0] & 0x7F
+    nb = (X // 96 + 1) * (Y // 96 + 1) * (Z // 8)  # blocks per volume
+    offs = np.frombuffer(whole, dtype="<u8", count=nb * Tn, offset=320)
+    base = 320 + 8 * nb * Tn
+    prev = 0
+    for t in range(Tn):
+        vol = oracle.synthetic_lf(X, Y, Z=Z, T=T, seed=0x4C464D05, t0=t, idx0=t * Z * X * Y)
+        assert np.array_equal(vol[0, 0], img[t, 0])
+        alone = oracle.encode(vol, header_version=0x80 | (8 + k), nnum=T, family="tiles")
+        end = int(offs[(t + 1) * nb - 1])
+        assert whole[base + prev:base + end] == alone[320 + 8 * nb:], t
+        prev = end
+        if t == 0:
+            assert oracle.encode(vol, header_version=0x80, nnum=T, family="tiles")[320 + 8 * nb:] == \
+                alone[320 + 8 * nb:]
+
