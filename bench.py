@@ -324,7 +324,7 @@ def inproc_leg(local, threads, ndevs):
                 runs.append((time.perf_counter() - t0) * 1e3)
             ok = None if e is None else (len(b) == e["size"] and hashlib.sha256(b).hexdigest() == e["sha256"])
             ms = min(runs)
-            out["gpus_%d" % len(devs)] = {"devices": devs, "Mpixel_per_s": round(px / ms / 1e3, 1),
+            out["workers_%d" % len(devs) if len(set(devs)) < len(devs) else "gpus_%d" % len(devs)] = {"devices": devs, "Mpixel_per_s": round(px / ms / 1e3, 1),
                                           "ms": round(ms, 2), "runs_ms": [round(x, 2) for x in runs],
                                           "verified": ok}
     finally:
@@ -524,6 +524,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_inproc:
         nvis = torch.cuda.device_count()
         legs = [[local]] + ([list(range(nvis))] if nvis > 1 else [])
+        if os.environ.get("LFM_BENCH_INPROC"):  # e.g. "0,0,0,0": four workers on one GPU (rehearsal)
+            legs = [[local], [int(x) for x in os.environ["LFM_BENCH_INPROC"].split(",")]]
         line["inproc"] = inproc_leg(local, threads, legs)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(threads=threads)

@@ -120,3 +120,24 @@ def test_bench_two_ranks_one_shared_lfm(gpu, tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["verified"]["ok"], line
+
+
+@pytest.mark.timeout(320)
+def test_bench_inproc_leg_four_workers(gpu, tmp_path):
+    """bench.py's `inproc` leg -- the drop-in writer (lfm_encoder_encode_multi,
+    what klb_imageIO::writeImage runs) on config 4 from host memory -- with
+    four workers mapped onto the one GPU (LFM_BENCH_INPROC=0,0,0,0): both the
+    one-device and the four-worker encodes give the oracle's cfg4 bytes, so
+    `--gpus 1` on an 8-GPU node times the same code path over 8 devices."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ, LFM_BENCH_INPROC="0,0,0,0", LFM_BZ2_GPU_BUDGET_MB="8192")
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1", "--warmup", "1", "--frames", "16",
+           "--no-decode", "--no-cpu-baseline", "--no-host-input", "--no-config5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    legs = line["inproc"]
+    assert legs["gpus_1"]["verified"] is True, legs
+    assert legs["workers_4"]["verified"] is True and legs["workers_4"]["devices"] == [0, 0, 0, 0], legs
