@@ -6,8 +6,12 @@
  * `numThreads`, writeImage / writeImageStackSlices / readImage /
  * readImageFull / readHeader.  The implementation is MI355X-native: the
  * predictor stage and the predictor selection run as HIP kernels on the GPU
- * (lfm_hip.h) for whole stacks at once; bzip2 runs on a host worker pool
- * with an in-order writer.
+ * (lfm_hip.h) for whole stacks at once, and so does bzip2: every block is
+ * compressed on the GPU, byte-identical to libbzip2 1.0.6 (the host library
+ * only takes the rare streams the device flags).  writeImage farms block-layer
+ * ranges over the node's GPUs (lfm_set_devices / LFM_GPUS; one device per
+ * rank in a one-process-per-GPU job) with an in-order writer; readImageFull
+ * decodes on the GPU (bzip2 decode + inverse predictor).
  */
 #ifndef LFM_KLB_IMAGE_IO_H
 #define LFM_KLB_IMAGE_IO_H

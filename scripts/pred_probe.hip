@@ -51,6 +51,40 @@ static float time_it(F launch, int it = 20)
     return ms / it;
 }
 
+// one launch at a time after a 1 GiB write (the 256 MiB Infinity Cache and
+// the L2s hold none of the kernel's input), as in the encoder where ~24 ms of
+// bzip2 work runs between two predictor launches
+static void* g_flush = nullptr;
+static unsigned long long* g_sink = nullptr;
+static bool g_clean_flush = false;  // read the 1 GiB instead (caches full of CLEAN lines)
+__global__ void read_flush(const v4u* __restrict__ a, size_t n, unsigned long long* sink)
+{
+    uint32_t x = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        x ^= a[i].x ^ a[i].w;
+    if (x == 0x12345678u) atomicAdd(sink, 1ull);
+}
+template <class F>
+static float time_cold(F launch, int it = 10)
+{
+    float tot = 0;
+    for (int i = 0; i < it; ++i) {
+        if (g_clean_flush)
+            hipLaunchKernelGGL(read_flush, dim3(2048), dim3(256), 0, 0, (const v4u*)g_flush, ((size_t)1 << 30) / 16,
+                               g_sink);
+        else
+            (void)hipMemsetAsync(g_flush, i & 0xFF, (size_t)1 << 30, 0);
+        (void)hipEventRecord(e0);
+        launch();
+        (void)hipEventRecord(e1);
+        (void)hipEventSynchronize(e1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        tot += ms;
+    }
+    return tot / it;
+}
+
 template <int PF>
 __global__ __launch_bounds__(256) void k_rows_nt(const v4u* __restrict__ a, v4u* __restrict__ b, int R, int nrows)
 {
@@ -75,6 +109,9 @@ int main(int argc, char** argv)
     uint16_t *in = nullptr, *ref = nullptr, *out = nullptr;
     unsigned long long* bad = nullptr;
     if (hipMalloc(&in, bytes) || hipMalloc(&ref, bytes) || hipMalloc(&out, bytes) || hipMalloc(&bad, 8)) return 1;
+    if (hipMalloc(&g_flush, (size_t)1 << 30) || hipMalloc(&g_sink, 8)) return 1;
+    (void)hipMemset(g_flush, 0x5a, (size_t)1 << 30);
+    g_clean_flush = argc > 3 && std::atoi(argv[3]) == 1;
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, in, n, 12345u);
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
@@ -92,6 +129,24 @@ int main(int argc, char** argv)
         return (long long)h;
     };
     const int reps = argc > 1 ? std::atoi(argv[1]) : 2;
+    // cold single launches: copy ceiling, round-2 ring, the product shapes
+    for (int rep = 0; rep < reps; ++rep) {
+        report("cold_rows_R8_pf4_ntst_copy", time_cold([&] {
+                   hipLaunchKernelGGL((k_rows_nt<4>), dim3(H * Z / 8), dim3(256), 0, 0, (const v4u*)in, (v4u*)out, 8,
+                                      H * Z);
+               }), -1);
+        p.out = out;
+        report("cold_vec_angleP4", time_cold([&] { (void)launch_vec<1, 4>(p, 0); }), -1);
+        report("cold_vec_copy", time_cold([&] { (void)launch_vec_shape<1, 0, 15, 1, 4, 1, 3>(p, 0); }), -1);
+        report("cold_vec_spaceP4", time_cold([&] { (void)launch_vec<2, 4>(p, 0); }), -1);
+        report("cold_vec_tilesP4", time_cold([&] { (void)launch_vec<0, 4>(p, 0); }), -1);
+        report("warm_vec_angleP4", time_it([&] { (void)launch_vec<1, 4>(p, 0); }), -1);
+        report("warm_rows_R8_pf4_ntst_copy", time_it([&] {
+                   hipLaunchKernelGGL((k_rows_nt<4>), dim3(H * Z / 8), dim3(256), 0, 0, (const v4u*)in, (v4u*)out, 8,
+                                      H * Z);
+               }), -1);
+    }
+    if (argc > 2 && std::atoi(argv[2]) == 0) return 0;  // cold probes only
     for (int rep = 0; rep < reps; ++rep) {
         report("rows_R8_pf4_ntst_copy", time_it([&] {
                    hipLaunchKernelGGL((k_rows_nt<4>), dim3(H * Z / 8), dim3(256), 0, 0, (const v4u*)in, (v4u*)out, 8,
