@@ -28,7 +28,9 @@ N > 1 (`verified` in the JSON line).  At N = 1 the same stack is also encoded
 from host memory (pinned and pageable), H2D inside the timed region:
 `host_input` (the PCIe-inclusive rate; `value` is always HBM-resident).
 
-At N = 1 two more legs follow (not the metric): `config5` -- four full
+At N = 1 more legs follow (not the metric): `configs_1_2` -- BASELINE
+configs 1 (img.tif, predictor off; beside the reference's own CPU path) and 2
+(512 x 512 space frame), bytes checked; `config5` -- four full
 t-volumes of config 5 (4096 x 4096 x 32 x 1 x 4, video, tiles) encoded from
 HBM into one .lfm (SHA-256 checked) and decoded back, the per-GPU rate of the
 config-5 round trip; `inproc` -- the drop-in multi-GPU writer
@@ -112,7 +114,20 @@ def cpu_baseline(seconds_budget=20.0, threads=None):
         nb1 += 1
     dt1 = time.perf_counter() - t1
     px1 = nb1 * 96 * 96 * 8
-    return {"value": px / dt / 1e6, "unit": "Mpixel/s", "cores": threads,
+    # BASELINE config 1 on the reference's CPU path: img.tif page 0 and the
+    # 29-page stack, request 8, one thread, the reference's bzip2 (as above)
+    tif = np.load(os.path.join(REPO, "tests", "golden", "img_tif.npz"))["img"]
+    cfg1 = {}
+    for name, im in (("page0", tif[0][None, None, None]), ("stack29", tif[None, None])):
+        reps = 20
+        t2 = time.perf_counter()
+        for _ in range(reps):
+            rb = O.encode(im, header_version=8, nnum=13, family="tiles")
+        ms = (time.perf_counter() - t2) * 1e3 / reps
+        px_i = int(np.prod(im.shape))
+        cfg1[name] = {"Mpixel_per_s": round(px_i / ms / 1e3, 2), "ms": round(ms, 3),
+                      "ratio": round(px_i * 2 / len(rb), 4)}
+    return {"value": px / dt / 1e6, "unit": "Mpixel/s", "cores": threads, "config1": cfg1,
             "kind": "reference" if "reference" in bz.kind else "port",
             "sample": "%dx%dx%d uint16 synthetic slab of the bench stack, request 8 (predictor off), 96x96x8 blocks, "
                       "bzip2 level 2 (%s), %d blocks, ratio %.3f" % (X, Y, zs, bz.kind, len(blocks),
@@ -293,6 +308,69 @@ def config5_leg(local, threads, nvol=4):
                     "upload of the payload and download of the pixels included)"}
 
 
+def _lfm_manifest(name):
+    path = os.path.join(REPO, "tests", "golden", "lfm_manifest.json")
+    try:
+        return {e["name"]: e for e in json.load(open(path))}.get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def small_configs_leg(local, threads, reps=20):
+    """BASELINE.md's per-config figures for the two small configs.
+    Config 1 (testData/img.tif page 0, 101 x 151, all zeros; and its 29-page
+    stack; request 8 = predictor off): this library's encode of the host
+    image, Mpixel/s and ratio, bytes checked (the reference's CPU path on the
+    same input is timed in cpu_baseline).
+    Config 2 (512 x 512, Nnum 13, space, auto): device-resident encode and the
+    predictor kernel's HBM fraction (a 0.5 MB frame: launch-latency bound)."""
+    out = {}
+    tif = np.load(os.path.join(REPO, "tests", "golden", "img_tif.npz"))["img"]
+    enc = lfm.Encoder(device=local, num_threads=threads)
+    try:
+        lfm.set_family("tiles")
+        for name, img in (("cfg1_imgtif_page0_req8", tif[0][None, None, None]),
+                          ("cfg1_imgtif_stack_req8", tif[None, None])):
+            e = _lfm_manifest(name)
+            px = int(np.prod(img.shape))
+            b, _ = enc.encode(img, header_version=8, nnum=13)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                b, _ = enc.encode(img, header_version=8, nnum=13)
+            ms = (time.perf_counter() - t0) * 1e3 / reps
+            ok = None if e is None else hashlib.sha256(b).hexdigest() == e["sha256"]
+            out[name] = {"shape_tczyx": list(img.shape), "Mpixel_per_s": round(px / ms / 1e3, 2),
+                         "ms": round(ms, 3), "ratio": round(px * 2 / len(b), 4), "verified": ok,
+                         "note": "host image -> in-memory .lfm (the reference's CPU path on the same input: "
+                                 "cpu_baseline.config1)"}
+        lfm.set_family("space")
+        e = _lfm_manifest("cfg2_512x512_space_auto")
+        d = torch.empty((1, 512, 512), dtype=torch.int16, device="cuda")
+        lfm.synth_device(d, 512, 512, 1, 13, seed=0x4C464D02)
+        torch.cuda.synchronize()
+        b, st = enc.encode(d, header_version=0, nnum=13)
+        pms, walls = [], []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            b, st = enc.encode(d, header_version=0, nnum=13)
+            walls.append((time.perf_counter() - t0) * 1e3)
+            pms.append(st["predict_ms"])
+        ms, kms = float(np.median(walls)), float(np.median(pms))
+        alg = 512 * 512 * 4
+        out["cfg2_512x512_space_auto"] = {
+            "Mpixel_per_s": round(512 * 512 / ms / 1e3, 2), "ms": round(ms, 3), "chosen_predictor": st["chosen"],
+            "ratio": round(512 * 512 * 2 / len(b), 4),
+            "verified": None if e is None else hashlib.sha256(b).hexdigest() == e["sha256"],
+            "predict_kernel_ms": round(kms, 4), "predict_frac_8TBs": round(alg / (kms / 1e3) / 8e12, 4),
+            "note": "one 512x512 frame: the encode is latency-bound (selection, one predictor launch, one bzip2 "
+                    "batch); the kernel moves 1 MiB, far below what fills the GPU"}
+    finally:
+        enc.close()
+        lfm.set_family(FAMILY)
+    return out
+
+
 def inproc_leg(local, threads, ndevs):
     """The drop-in multi-GPU writer -- lfm_encoder_encode_multi, the block
     scheduler behind klb_imageIO::writeImage / writeKLBstack -- on config 4
@@ -345,6 +423,7 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-host-input", action="store_true")
     ap.add_argument("--no-config5", action="store_true")
+    ap.add_argument("--no-small", action="store_true")
     ap.add_argument("--no-inproc", action="store_true")
     args = ap.parse_args()
 
@@ -519,6 +598,8 @@ def main():
                           "first_ms": round(dlist[0], 1), "runs_ms": [round(x, 1) for x in dlist],
                           "exact": exact,
                           "path": "GPU bzip2 decode + GPU inverse predictor (host libbz2 only for flagged streams, %d threads)" % threads}
+    if rank == 0 and world == 1 and not args.no_small:
+        line["configs_1_2"] = small_configs_leg(local, threads)
     if rank == 0 and world == 1 and not args.no_config5:
         line["config5"] = config5_leg(local, threads)
     if rank == 0 and world == 1 and not args.no_inproc:
