@@ -475,6 +475,10 @@ def main():
         stats.append(st)
         return b
 
+    # LFM_BENCH_FORCE_K=k (diagnostic, not the metric): skip the selection and
+    # force predictor k, to see what the selection costs the pipeline
+    hv_req = 8 + int(os.environ["LFM_BENCH_FORCE_K"]) if os.environ.get("LFM_BENCH_FORCE_K") else 0
+
     def run(nsteps, stats):
         """nsteps encodes of the stack, pipelined (lfm_encoder_submit / wait):
         encode i's kernels run while encode i-1's last payload copies drain
@@ -485,7 +489,7 @@ def main():
             # auto request: the submit selects on the stack's frame 0 (its own
             # frame 0 at rank 0, handed in on the others) on the encoder's
             # stream, after the previous encode's kernels
-            ticket = enc.submit(d_img, z0, header_version=0, nnum=T, select_frame=sel_frame)
+            ticket = enc.submit(d_img, z0, header_version=hv_req, nnum=T, select_frame=sel_frame)
             if pending is not None:
                 b = finish(pending, stats)
             pending = ticket

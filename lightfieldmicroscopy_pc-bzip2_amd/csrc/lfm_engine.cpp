@@ -524,25 +524,35 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     const int p = par_;
     Inflight& f = fly_[p];
     if (f.th.joinable()) f.th.join();  // the encode before last used this buffer set
-    // Auto-selection (klb_imageIO.cpp:2316-2360) runs FIRST, before waiting for
-    // the previous encode's release: its short kernels interleave with that
-    // encode's GPU bzip2 instead of adding to this encode's critical path.  The
-    // request then becomes the forced 8 + k (video bit kept) for the predictor
-    // stage; the bytes are the same.
+    // Auto-selection (klb_imageIO.cpp:2316-2360) on the encoder's stream, once
+    // the previous encode's kernels are done (its release); the request then
+    // becomes the forced 8 + k (video bit kept) for the predictor stage, the
+    // bytes are the same.  LFM_PRESELECT_EARLY=1 runs it before that wait
+    // instead, interleaved with the previous encode's GPU bzip2: same
+    // throughput within noise (10 966-11 361 vs 11 046-11 047 Mpixel/s, same
+    // box), but its wall time is then mostly queueing (4-8 ms) and the
+    // predictor after it runs 5-10 % slower (more dirty lines in the caches).
+    static const bool early = std::getenv("LFM_PRESELECT_EARLY") && std::atoi(std::getenv("LFM_PRESELECT_EARLY")) == 1;
     const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
     const int req0 = h.headerVersion & 0x7F;
     int pre_k = -1;
     float pre_ent[8] = {0};
     double pre_ms = 0.0;
-    if (gpu_bz && req0 < NUM_PREDICTORS && h.getBytesPerPixel() == 2 && h.Nnum > 0) {
+    auto select_now = [&]() -> int {
         auto ts0 = clk::now();
         if (int rc = preselect(img, dev, h, slab ? *slab : whole, &pre_k, pre_ent)) return rc;
         pre_ms = ms_since(ts0);
         h.headerVersion = (uint8_t)((h.headerVersion & 0x80) | (8 + pre_k));
         if (trace) ts("selected");
-    }
+        return 0;
+    };
+    const bool pre = gpu_bz && req0 < NUM_PREDICTORS && h.getBytesPerPixel() == 2 && h.Nnum > 0;
+    if (pre && early)
+        if (int rc = select_now()) return rc;
     fly_[p ^ 1].wait_release();        // the previous encode is in its tail
     if (trace) ts("released");
+    if (pre && !early)
+        if (int rc = select_now()) return rc;
     f.ticket = next_ticket_++;
     f.rc = 0;
     std::memset(&f.st, 0, sizeof(f.st));
