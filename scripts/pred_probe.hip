@@ -56,7 +56,12 @@ static float time_it(F launch, int it = 20)
 // bzip2 work runs between two predictor launches
 static void* g_flush = nullptr;
 static unsigned long long* g_sink = nullptr;
-static bool g_clean_flush = false;  // read the 1 GiB instead (caches full of CLEAN lines)
+static int g_flush_mode = 0;  // 0: hipMemset (dirty lines), 1: read the 1 GiB (clean lines), 2: nt stores
+__global__ void nt_fill(v4u* __restrict__ a, size_t n, uint32_t v)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(v4u{v, v, v, v}, &a[i]);
+}
 __global__ void read_flush(const v4u* __restrict__ a, size_t n, unsigned long long* sink)
 {
     uint32_t x = 0;
@@ -69,9 +74,11 @@ static float time_cold(F launch, int it = 10)
 {
     float tot = 0;
     for (int i = 0; i < it; ++i) {
-        if (g_clean_flush)
+        if (g_flush_mode == 1)
             hipLaunchKernelGGL(read_flush, dim3(2048), dim3(256), 0, 0, (const v4u*)g_flush, ((size_t)1 << 30) / 16,
                                g_sink);
+        else if (g_flush_mode == 2)
+            hipLaunchKernelGGL(nt_fill, dim3(2048), dim3(256), 0, 0, (v4u*)g_flush, ((size_t)1 << 30) / 16, (uint32_t)i);
         else
             (void)hipMemsetAsync(g_flush, i & 0xFF, (size_t)1 << 30, 0);
         (void)hipEventRecord(e0);
@@ -111,7 +118,7 @@ int main(int argc, char** argv)
     if (hipMalloc(&in, bytes) || hipMalloc(&ref, bytes) || hipMalloc(&out, bytes) || hipMalloc(&bad, 8)) return 1;
     if (hipMalloc(&g_flush, (size_t)1 << 30) || hipMalloc(&g_sink, 8)) return 1;
     (void)hipMemset(g_flush, 0x5a, (size_t)1 << 30);
-    g_clean_flush = argc > 3 && std::atoi(argv[3]) == 1;
+    g_flush_mode = argc > 3 ? std::atoi(argv[3]) : 0;
     hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, in, n, 12345u);
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
