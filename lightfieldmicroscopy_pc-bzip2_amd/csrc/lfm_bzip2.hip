@@ -808,6 +808,361 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     }
 }
 
+// Hand-written chunk sort, LDS merge path (LFM_CS_ALGO=1; measured slower than
+// the rocPRIM kernel above: bz_bwt_ms 13.0 vs 11.0-11.5, same box).  Built to
+// issue fewer VALU instructions than rocPRIM's ~327 lane-ops per rotation; it
+// does (~300), but its blocked 16-byte LDS writes and random merge reads run
+// 8.6 bank-conflict cycles per LDS instruction against rocPRIM's 3.1
+// (profiles/r03_pmc_chunk_sorts.txt).
+//  - every lane owns IPT = 8 rotations (striped loads, keys rebuilt from the
+//    text), sorted in registers by Batcher's 19-exchange network;
+//  - merge levels L = 8 .. NI/2 through one LDS key / value array: each lane
+//    finds its 8 outputs' start on the merge path (log2 L + 1 probes) and
+//    merges them sequentially, tracking LDS indices only -- the values are
+//    gathered once per level by index, not selected at every step;
+//  - the levels whose pairs of runs lie inside one wave's 8 x 64 items need
+//    no s_barrier (one wave's LDS operations execute in order): only the last
+//    log2(TH / 64) levels synchronise the workgroup.
+// Padding slots (j >= m) sort as key ~0 with value kPad; a real rotation whose
+// 8-byte prefix is all ones (possible only in the chunk of the last bucket)
+// ties with them, so such a chunk compacts its real values below m afterwards.
+constexpr uint32_t kPad = 0xFFFFFFFFu;  // never a value: rotation starts are < 2^24
+
+__device__ __forceinline__ void wave_lds_order()
+{
+    // a compiler barrier between one wave's LDS writes and its later reads of
+    // other lanes' slots (the hardware executes a wave's DS instructions in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int I, int J>
+__device__ __forceinline__ void cs_exchange(uint64_t* k, uint32_t* v)
+{
+    const bool sw = k[I] > k[J];
+    const uint64_t a = k[I], b = k[J];
+    const uint32_t x = v[I], y = v[J];
+    k[I] = sw ? b : a;
+    k[J] = sw ? a : b;
+    v[I] = sw ? y : x;
+    v[J] = sw ? x : y;
+}
+
+template <int TH, int IPT>
+__global__ __launch_bounds__(TH) void bwt_chunk_msort(Batch B, const uint32_t* __restrict__ cbp,
+                                                      const uint32_t* __restrict__ cep, uint32_t nch, uint32_t per)
+{
+    static_assert(IPT == 8 && TH >= 64 && (TH & (TH - 1)) == 0, "8 items per lane, power-of-two workgroup");
+    constexpr uint32_t NI = TH * IPT;
+    constexpr uint32_t WI = 64 * IPT;  // one wave's items
+    __shared__ uint64_t sk[NI];
+    __shared__ uint32_t sv[NI];
+    __shared__ uint32_t s_nmax;
+    const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
+    if (c >= nch) return;
+    const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
+    const uint32_t s = cb / B.cap, n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
+    if (t == 0) s_nmax = 0;
+    uint64_t k[IPT];
+    uint32_t v[IPT];
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = q * TH + t;
+        v[q] = j < m ? B.vals_a[cb + j] : kPad;
+    }
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const bool real = v[q] != kPad;
+        k[q] = real ? rot_key8_fast(T, n, v[q] & kIdxMask) : ~0ull;
+        nmax += (real && k[q] == ~0ull) ? 1u : 0u;
+    }
+    // Batcher's odd-even merge sort of 8
+    cs_exchange<0, 1>(k, v); cs_exchange<2, 3>(k, v); cs_exchange<4, 5>(k, v); cs_exchange<6, 7>(k, v);
+    cs_exchange<0, 2>(k, v); cs_exchange<1, 3>(k, v); cs_exchange<4, 6>(k, v); cs_exchange<5, 7>(k, v);
+    cs_exchange<1, 2>(k, v); cs_exchange<5, 6>(k, v);
+    cs_exchange<0, 4>(k, v); cs_exchange<1, 5>(k, v); cs_exchange<2, 6>(k, v); cs_exchange<3, 7>(k, v);
+    cs_exchange<2, 4>(k, v); cs_exchange<3, 5>(k, v);
+    cs_exchange<1, 2>(k, v); cs_exchange<3, 4>(k, v); cs_exchange<5, 6>(k, v);
+    const uint32_t e0 = t * IPT;
+#pragma unroll 1
+    for (uint32_t L = IPT; L < NI; L *= 2) {
+        // this lane's run goes back to LDS once the previous level's readers of
+        // those slots (its pair of runs: L items) are done
+        if (L > IPT) {
+            if (L <= WI) wave_lds_order();
+            else __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < IPT; q += 2) {
+            *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
+        }
+        *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
+        *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
+        if (2 * L <= WI) wave_lds_order();
+        else __syncthreads();
+        // merge path: outputs d .. d + IPT - 1 of the pair (runs A, B at pb)
+        const uint32_t pb = e0 & ~(2 * L - 1), d = e0 - pb;
+        const uint64_t* A = sk + pb;
+        const uint64_t* Bk = A + L;
+        uint32_t lo = d > L ? d - L : 0u, hi = d < L ? d : L;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (A[mid] <= Bk[d - 1 - mid]) lo = mid + 1;
+            else hi = mid;
+        }
+        uint32_t i = lo, j = d - lo;
+        uint64_t a = A[min(i, L - 1)], b = Bk[min(j, L - 1)];
+        uint32_t idx[IPT];
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            const bool ta = i < L && (j >= L || a <= b);
+            k[q] = ta ? a : b;
+            idx[q] = ta ? pb + i : pb + L + j;
+            i += ta ? 1u : 0u;
+            j += ta ? 0u : 1u;
+            if (q + 1 < IPT) {
+                const uint64_t x = sk[ta ? pb + min(i, L - 1) : pb + L + min(j, L - 1)];
+                a = ta ? x : a;
+                b = ta ? b : x;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) v[q] = sv[idx[q]];
+    }
+    if (nmax) atomicAdd(&s_nmax, nmax);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < IPT; q += 2) *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
+    *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
+    *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
+    __syncthreads();
+    const uint32_t cm = s_nmax;
+    if (cm && m < NI) {
+        // slots [m - cm, NI) all hold key ~0: move the cm real values below m
+        if (t == 0) {
+            uint32_t w = m - cm;
+            for (uint32_t q = m - cm; q < NI && w < m; ++q)
+                if (sv[q] != kPad) sv[w++] = sv[q];
+        }
+        __syncthreads();
+    }
+    uint32_t nt = 0;
+    for (uint32_t q = t; q < m; q += TH) {
+        const uint64_t x = sk[q];
+        const bool f = (q > 0 && sk[q - 1] == x) || (q + 1 < m && sk[q + 1] == x);
+        B.sa[cb + q] = sv[q];
+        B.uflag[cb + q] = f ? 1 : 0;
+        nt += f ? 1u : 0u;
+    }
+    if (__any(nt)) {
+        for (int dd = 32; dd > 0; dd >>= 1) nt += __shfl_xor(nt, dd);
+        if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[s], nt);
+    }
+}
+
+// Register bitonic chunk sort (LFM_CS_ALGO=2; measured slower still: bz_bwt_ms
+// 15.2, ~450 VALU lane-ops per rotation -- the first round is bound by LDS and
+// VALU together, and rocPRIM's merge sort balances the two best of the three).
+// Element e = t * 8 + q sits in
+// register q of lane t for the whole sort: exchanges at item distance 1, 2, 4
+// are in-lane, at 8 .. 256 cross-lane (DPP quad_perm for lane xor 1 / 2,
+// ds_swizzle for 4 / 8, v_permlane16/32_swap for 16 / 32: no LDS bank and no
+// dependent LDS chains), and only distances >= 512 (across waves) go through
+// LDS.  Oblivious: the same instruction stream for every chunk.
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x)
+{
+    if constexpr (M == 1) return __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 10));  // xor M within 32 lanes
+}
+
+// both members of the pair (lane, lane ^ M) for M = 16 / 32: lo = the element
+// of the lane with bit M clear, hi = the other
+template <int M>
+__device__ __forceinline__ void lane_pair(uint32_t x, uint32_t& lo, uint32_t& hi)
+{
+    if constexpr (M == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        lo = r[0];
+        hi = r[1];
+    } else {
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        lo = r[0];
+        hi = r[1];
+    }
+}
+
+template <int I, int J>
+__device__ __forceinline__ void cs_exchange_dir(uint64_t* k, uint32_t* v, bool desc)
+{
+    const bool sw = (k[I] > k[J]) != desc;  // equal keys may swap: both stay in the lane
+    const uint64_t a = k[I], b = k[J];
+    const uint32_t x = v[I], y = v[J];
+    k[I] = sw ? b : a;
+    k[J] = sw ? a : b;
+    v[I] = sw ? y : x;
+    v[J] = sw ? x : y;
+}
+
+template <int D>  // in-lane half-cleaner at item distance D (1, 2, 4)
+__device__ __forceinline__ void bs_inlane(uint64_t* k, uint32_t* v, bool desc)
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if ((q & D) == 0) {
+            const int p = q | D;
+            const bool sw = (k[q] > k[p]) != desc;
+            const uint64_t a = k[q], b = k[p];
+            const uint32_t x = v[q], y = v[p];
+            k[q] = sw ? b : a;
+            k[p] = sw ? a : b;
+            v[q] = sw ? y : x;
+            v[p] = sw ? x : y;
+        }
+}
+
+template <int M>  // cross-lane half-cleaner with lane ^ M (M = 1 .. 32)
+__device__ __forceinline__ void bs_xlane(uint64_t* k, uint32_t* v, bool keep_min, bool lower)
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t klo = (uint32_t)k[q], khi = (uint32_t)(k[q] >> 32);
+        if constexpr (M <= 8) {
+            const uint64_t tk = ((uint64_t)lane_xor<M>(khi) << 32) | lane_xor<M>(klo);
+            const uint32_t tv = lane_xor<M>(v[q]);
+            // ties keep their own element on both sides (no duplicate)
+            const bool take = keep_min ? tk < k[q] : k[q] < tk;
+            k[q] = take ? tk : k[q];
+            v[q] = take ? tv : v[q];
+        } else {
+            uint32_t l0, h0, l1, h1, lv, hv;
+            lane_pair<M>(klo, l0, h0);
+            lane_pair<M>(khi, l1, h1);
+            lane_pair<M>(v[q], lv, hv);
+            const uint64_t lk = ((uint64_t)l1 << 32) | l0, hk = ((uint64_t)h1 << 32) | h0;
+            // the lower lane's element is lk; keep min(lk, hk) or max (ties: each its own)
+            const bool c = lk > hk;
+            const bool pick_hi = keep_min ? c : !c;
+            const bool same = lk == hk;
+            const bool hi_side = !lower;
+            const bool take_hi = same ? hi_side : pick_hi;
+            k[q] = take_hi ? hk : lk;
+            v[q] = take_hi ? hv : lv;
+        }
+    }
+}
+
+template <int TH, int LOGN, int K, int J>
+__device__ __forceinline__ void bs_stages(uint64_t* k, uint32_t* v, uint32_t t, uint64_t* sk, uint32_t* sv)
+{
+    if constexpr (K <= LOGN) {
+        const bool desc = K == LOGN ? false : ((t >> (K - 3)) & 1u) != 0;
+        if constexpr (J < 3) {
+            bs_inlane<1 << J>(k, v, desc);
+        } else if constexpr (J < 9) {
+            const bool lower = ((t >> (J - 3)) & 1u) == 0;
+            bs_xlane<1 << (J - 3)>(k, v, lower != desc, lower);
+        } else {
+            // across waves: through LDS (lane t ^ 2^(J-3), same register)
+            const uint32_t e0 = t * 8;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
+            *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
+            *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
+            __syncthreads();
+            const uint32_t p0 = e0 ^ (1u << J);
+            const bool lower = (e0 & (1u << J)) == 0;
+            const bool keep_min = lower != desc;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t tk = sk[p0 + q];
+                const uint32_t tv = sv[p0 + q];
+                const bool take = keep_min ? tk < k[q] : k[q] < tk;
+                k[q] = take ? tk : k[q];
+                v[q] = take ? tv : v[q];
+            }
+        }
+        if constexpr (J > 0) bs_stages<TH, LOGN, K, J - 1>(k, v, t, sk, sv);
+        else bs_stages<TH, LOGN, K + 1, K>(k, v, t, sk, sv);
+    }
+}
+
+template <int TH>
+__global__ __launch_bounds__(TH) void bwt_chunk_bsort(Batch B, const uint32_t* __restrict__ cbp,
+                                                      const uint32_t* __restrict__ cep, uint32_t nch, uint32_t per)
+{
+    constexpr int IPT = 8;
+    constexpr uint32_t NI = TH * IPT;
+    constexpr int LOGN = TH == 128 ? 10 : TH == 256 ? 11 : 12;
+    static_assert((1u << LOGN) == NI, "power-of-two chunk capacity");
+    __shared__ uint64_t sk[NI];
+    __shared__ uint32_t sv[NI];
+    __shared__ uint32_t s_nmax;
+    const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
+    if (c >= nch) return;
+    const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
+    const uint32_t s = cb / B.cap, n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
+    if (t == 0) s_nmax = 0;
+    uint64_t k[IPT];
+    uint32_t v[IPT];
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = q * TH + t;
+        v[q] = j < m ? B.vals_a[cb + j] : kPad;
+    }
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const bool real = v[q] != kPad;
+        k[q] = real ? rot_key8_fast(T, n, v[q] & kIdxMask) : ~0ull;
+        nmax += (real && k[q] == ~0ull) ? 1u : 0u;
+    }
+    // lane runs of 8, ascending in even lanes and descending in odd ones
+    const bool d3 = (t & 1u) != 0;
+    cs_exchange_dir<0, 1>(k, v, d3); cs_exchange_dir<2, 3>(k, v, d3); cs_exchange_dir<4, 5>(k, v, d3); cs_exchange_dir<6, 7>(k, v, d3);
+    cs_exchange_dir<0, 2>(k, v, d3); cs_exchange_dir<1, 3>(k, v, d3); cs_exchange_dir<4, 6>(k, v, d3); cs_exchange_dir<5, 7>(k, v, d3);
+    cs_exchange_dir<1, 2>(k, v, d3); cs_exchange_dir<5, 6>(k, v, d3);
+    cs_exchange_dir<0, 4>(k, v, d3); cs_exchange_dir<1, 5>(k, v, d3); cs_exchange_dir<2, 6>(k, v, d3); cs_exchange_dir<3, 7>(k, v, d3);
+    cs_exchange_dir<2, 4>(k, v, d3); cs_exchange_dir<3, 5>(k, v, d3);
+    cs_exchange_dir<1, 2>(k, v, d3); cs_exchange_dir<3, 4>(k, v, d3); cs_exchange_dir<5, 6>(k, v, d3);
+    bs_stages<TH, LOGN, 4, 3>(k, v, t, sk, sv);
+    if (nmax) atomicAdd(&s_nmax, nmax);
+    const uint32_t e0 = t * IPT;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < IPT; q += 2) *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
+    *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
+    *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
+    __syncthreads();
+    const uint32_t cm = s_nmax;
+    if (cm && m < NI) {
+        if (t == 0) {
+            uint32_t w = m - cm;
+            for (uint32_t q = m - cm; q < NI && w < m; ++q)
+                if (sv[q] != kPad) sv[w++] = sv[q];
+        }
+        __syncthreads();
+    }
+    uint32_t nt = 0;
+    for (uint32_t q = t; q < m; q += TH) {
+        const uint64_t x = sk[q];
+        const bool f = (q > 0 && sk[q - 1] == x) || (q + 1 < m && sk[q + 1] == x);
+        B.sa[cb + q] = sv[q];
+        B.uflag[cb + q] = f ? 1 : 0;
+        nt += f ? 1u : 0u;
+    }
+    if (__any(nt)) {
+        for (int dd = 32; dd > 0; dd >>= 1) nt += __shfl_xor(nt, dd);
+        if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[s], nt);
+    }
+}
+
 // the first-round key of rotation i of stream s: its 8-byte prefix, big endian
 __device__ __forceinline__ uint64_t rot_key8(const Batch& B, uint32_t s, uint32_t i)
 {
@@ -2878,6 +3233,40 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             return dim3(cs_xcd ? 8 * per : nc);
         };
         uint32_t per = 0;
+        // chunk sorts: the rocPRIM block merge sort below (default), or the
+        // hand-written ones (LFM_CS_ALGO=1 LDS merge path, 2 register bitonic;
+        // both measured slower)
+        static const int cs_algo = [] {
+            const char* e = std::getenv("LFM_CS_ALGO");
+            const int x = e ? std::atoi(e) : 0;
+            return x >= 0 && x <= 2 ? x : 0;
+        }();
+        if (cs_algo) {
+            const void* fk[3];
+            if (cs_algo == 2) {
+                fk[0] = (const void*)bwt_chunk_bsort<kTinyCap / 8>;
+                fk[1] = (const void*)bwt_chunk_bsort<kSmallCap / 8>;
+                fk[2] = (const void*)bwt_chunk_bsort<kBigCap / 8>;
+            } else {
+                fk[0] = (const void*)bwt_chunk_msort<kTinyCap / 8, 8>;
+                fk[1] = (const void*)bwt_chunk_msort<kSmallCap / 8, 8>;
+                fk[2] = (const void*)bwt_chunk_msort<kBigCap / 8, 8>;
+            }
+            const uint32_t cls_n[3] = {nch[5], nch[0], nch[1]};
+            uint32_t* const cls_b[3] = {CL.b[3], CL.b[0], CL.b[1]};
+            uint32_t* const cls_e[3] = {CL.e[3], CL.e[0], CL.e[1]};
+            const uint32_t cls_th[3] = {kTinyCap / 8, kSmallCap / 8, kBigCap / 8};
+            for (int q = 0; q < 3; ++q) {
+                if (!cls_n[q]) continue;
+                const dim3 g = cs_grid(cls_n[q], per);
+                const uint32_t* cbq = cls_b[q];
+                const uint32_t* ceq = cls_e[q];
+                uint32_t nq = cls_n[q];
+                void* args[] = {&B, &cbq, &ceq, &nq, &per};
+                if (hipLaunchKernel(fk[q], g, dim3(cls_th[q]), args, 0, st) != hipSuccess) return LFM_HIP_ERUNTIME;
+            }
+            nch[5] = nch[0] = nch[1] = 0;  // done: only the rocPRIM segmented class below
+        }
         if (nch[5]) {
             const dim3 g = cs_grid(nch[5], per);
             hipLaunchKernelGGL((bwt_chunk_sort<kTinyCap / kCsItems, kCsItems>), g, dim3(kTinyCap / kCsItems), 0, st, B,
