@@ -122,6 +122,7 @@ struct Batch {
     uint32_t* out_bytes;
     uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
     uint32_t* wide_cnt;
+    uint32_t tie_direct;     // chunk sorts resolve runs of equal prefixes from the text (LFM_TIE_DIRECT)
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -721,6 +722,56 @@ __global__ __launch_bounds__(256) void bwt_chunk_keys(Batch B, const uint32_t* _
     for (uint32_t j = cb + threadIdx.x; j < ce; j += 256) B.keys_a[j] = rot_key8_fast(T, n, B.vals_a[j] & kIdxMask);
 }
 
+// Runs of rotations whose 8-byte prefixes are equal, resolved inside the
+// chunk sort when short: at most kTieRunMax rotations, ordered by insertion
+// on their cyclic text from byte kKeyBytes on, kTieCmpBytes at most per
+// comparison (bzip2 orders the rotations of the block lexicographically).  A
+// longer run, or one with a comparison still equal after kTieCmpBytes, keeps
+// its flags for the device-wide tie rounds, whose result does not depend on
+// the order the run is left in.
+constexpr uint32_t kTieRunMax = 32;
+constexpr uint32_t kTieCmpBytes = 64;
+
+// -1 / 1: rotation i sorts before / after rotation j, given equal first
+// kKeyBytes bytes; 0: still equal after kTieCmpBytes more
+__device__ __forceinline__ int tie_cmp(const uint8_t* __restrict__ T, uint32_t n, uint32_t i, uint32_t j)
+{
+    uint32_t a = (i + kKeyBytes) % n, b = (j + kKeyBytes) % n;
+    for (uint32_t d = 0; d < kTieCmpBytes; d += 8) {
+        const uint64_t ka = rot_key8_fast(T, n, a), kb = rot_key8_fast(T, n, b);
+        if (ka != kb) return ka < kb ? -1 : 1;
+        a = (a + 8) % n;
+        b = (b + 8) % n;
+    }
+    return 0;
+}
+
+// the run of prefix K starting at sorted position pos of a chunk (values sv,
+// still-tied flags fl in LDS, m positions): sort it and clear its flags
+__device__ void tie_run_sort(uint32_t* sv, uint8_t* fl, uint32_t pos, uint32_t m, uint64_t K,
+                             const uint8_t* __restrict__ T, uint32_t n)
+{
+    uint32_t e = pos + 1;
+    while (e < m && e - pos <= kTieRunMax && fl[e] && rot_key8_fast(T, n, sv[e] & kIdxMask) == K) ++e;
+    if (e - pos > kTieRunMax) return;
+    for (uint32_t x = pos + 1; x < e; ++x) {
+        const uint32_t vx = sv[x];
+        uint32_t y = x;
+        while (y > pos) {
+            const int c = tie_cmp(T, n, sv[y - 1] & kIdxMask, vx & kIdxMask);
+            if (c == 0) {  // undecided: the run stays flagged (same elements, any order)
+                sv[y] = vx;
+                return;
+            }
+            if (c < 0) break;
+            sv[y] = sv[y - 1];
+            --y;
+        }
+        sv[y] = vx;
+    }
+    for (uint32_t x = pos; x < e; ++x) fl[x] = 0;
+}
+
 // The chunk's keys / values are loaded striped (element q * TH + t: coalesced),
 // sorted (rocPRIM block merge sort: thread t ends with sorted positions
 // t * IPT .. t * IPT + IPT - 1), the still-tied flags come from the
@@ -797,10 +848,27 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
         if constexpr (IPT == 8) *(uint64_t*)&sm.x.fl[t * IPT] = fpack;
         else *(uint32_t*)&sm.x.fl[t * IPT] = (uint32_t)fpack;
     }
-    __syncthreads();
+    // runs of equal 8-byte prefixes (~0.02 % of rotations, nearly always
+    // pairs): sorted here by their text from byte 8 on, so the device-wide tie
+    // rounds -- dozens of tiny kernels and host round trips -- mostly find
+    // nothing left.  The thread owning a run's first position sorts it.
+    if (__syncthreads_or(nt != 0)) {
+        if (B.tie_direct) {
+#pragma unroll
+            for (int q = 0; q < IPT; ++q) {
+                const uint32_t pos = t * IPT + q;
+                const uint64_t lo = q ? k[q - 1] : kprev;
+                if (((fpack >> (8 * q)) & 1u) && (pos == 0 || lo != k[q])) tie_run_sort(sm.x.sv, sm.x.fl, pos, m, k[q], T, n);
+            }
+        }
+        __syncthreads();
+        nt = 0;
+    }
     for (uint32_t j = t; j < m; j += TH) {
+        const uint8_t f = sm.x.fl[j];
         B.sa[cb + j] = sm.x.sv[j];
-        B.uflag[cb + j] = sm.x.fl[j];
+        B.uflag[cb + j] = f;
+        nt += f;
     }
     if (__any(nt)) {
         for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
@@ -1283,9 +1351,14 @@ __global__ __launch_bounds__(1024) void bwt_rank0(Batch B)
         const uint32_t j = j0 + t;
         bool head = false, next_head = true;
         if (j < n) {
+            // a slot joins its predecessor's group only while the chunk sort
+            // left it flagged: runs it resolved (tie_run_sort) are final.
+            // Both flags are read before the barrier ahead of the rewrite.
+            const bool fj = B.uflag[o + j] != 0;
+            const bool fn = j + 1 < n && B.uflag[o + j + 1] != 0;
             const uint64_t k = K(j);
-            head = j == 0 || k != K(j - 1);
-            next_head = j + 1 >= n || K(j + 1) != k;
+            head = j == 0 || !fj || k != K(j - 1);
+            next_head = j + 1 >= n || !fn || K(j + 1) != k;
         }
         uint32_t v = head ? j : 0u;
         for (int off = 1; off < 64; off <<= 1) {
@@ -3146,6 +3219,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.sel_cap = (uint32_t)align_up(B.cap / kGSize + 8, 64);
     B.level = level;
     B.nblock_max = 100000u * level - 19u;
+    static const uint32_t tie_direct = !(std::getenv("LFM_TIE_DIRECT") && std::atoi(std::getenv("LFM_TIE_DIRECT")) == 0);
+    B.tie_direct = tie_direct;
     if (ws_bytes < lfm_hip_bzip2_workspace_bytes(count, raw_cap)) return LFM_HIP_EINVAL;
     const size_t N = (size_t)count * B.cap;
     if (N >= (1ull << 32)) return LFM_HIP_EINVAL;
@@ -3314,6 +3389,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     uint32_t* d_cnt2 = d_cnt + 1;
     // text rounds over the tied list (group keys: u64 per entry in the rank
     // area, group index / bounds in the mtfv area -- both free here)
+    bool none_left = false;  // a count read 0 and no kernel ran since: skip the later reads
+    uint32_t first_ties = 0;  // rotations still tied after the chunk sorts (LFM_BZ2_STATS)
     {
         uint64_t* gk = (uint64_t*)B.rank;
         uint32_t* bnd = (uint32_t*)B.mtfv;
@@ -3324,7 +3401,12 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
                 e = hipErrorUnknown;
                 break;
             }
-            if (cnt == 0 || (size_t)cnt * 4 > N) break;
+            if (r == 0) first_ties = cnt;
+            if (cnt == 0) {  // nothing tied (the usual case once the chunk sorts resolve their runs)
+                none_left = true;
+                break;
+            }
+            if ((size_t)cnt * 4 > N) break;
             unsigned gbits = 1;
             while ((1u << gbits) < cnt) ++gbits;
             // group index above the text bytes in one 64-bit key: fewer text
@@ -3348,8 +3430,9 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         // ties left (long repeats): ranks of every rotation for doubling
         uint32_t cnt = 0;
-        if (e == hipSuccess && (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                                hipStreamSynchronize(st) != hipSuccess))
+        if (e == hipSuccess && !none_left &&
+            (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+             hipStreamSynchronize(st) != hipSuccess))
             e = hipErrorUnknown;
         if (e == hipSuccess && cnt > 0) {
             // group bounds of the remaining list: from the last text keys, or
@@ -3379,7 +3462,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     // doubling rounds over what the text rounds left (long repeats only)
     uint32_t h = covered;
     const uint32_t max_n = B.cap;
-    while (e == hipSuccess) {
+    while (e == hipSuccess && !none_left) {
         uint32_t cnt = 0;
         if (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess) {
@@ -3477,8 +3560,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (stats) {
         uint32_t c[8] = {};
         if (hipMemcpyAsync(c, d_cnt, 32, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
-            std::fprintf(stderr, "lfm_bzip2 stats: %u streams, %u with u64 Huffman heaps, Huffman retries %u\n", count,
-                         c[3], c[4]);
+            std::fprintf(stderr, "lfm_bzip2 stats: %u streams, %u with u64 Huffman heaps, Huffman retries %u, "
+                         "tied after the chunk sorts %u\n", count, c[3], c[4], first_ties);
     }
     std::vector<uint32_t> nbytes(count);
     if (hipMemcpyAsync(nbytes.data(), B.out_bytes, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -320,6 +320,18 @@ def _bz2_cases():
         "long_repeat_lowalpha": np.concatenate([np.tile(rng.integers(0, 4, 3000, dtype=np.uint8), 9),
                                                 np.array([9, 9], np.uint8)]),
     }
+    # runs of equal 8-byte prefixes resolved inside the chunk sort (pairs and
+    # triples over a 4-symbol alphabet), at and past its run limit of 32 (a
+    # 20-byte motif 32 / 33 times), and past its 64-byte compare limit (a
+    # 200-byte block three times): the latter two go to the tie rounds
+    cases["alpha4"] = rng.integers(0, 4, 90000, dtype=np.uint8)
+    for reps in (32, 33):
+        motif = rng.integers(0, 256, 20, dtype=np.uint8)
+        cases["motif%d" % reps] = np.concatenate(
+            [np.concatenate([motif, rng.integers(0, 256, 50, dtype=np.uint8)]) for _ in range(reps)])
+    blk = rng.integers(0, 256, 200, dtype=np.uint8)
+    cases["tie_past_compare"] = np.concatenate(
+        [np.concatenate([blk, rng.integers(0, 256, 300, dtype=np.uint8)]) for _ in range(3)])
     runs = []
     for L in (1, 2, 3, 4, 5, 254, 255, 256, 259, 510, 511, 1000):
         runs.append(np.full(L, L % 251, np.uint8))
