@@ -123,6 +123,7 @@ struct Batch {
     uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
     uint32_t* wide_cnt;
     uint32_t tie_direct;     // chunk sorts resolve runs of equal prefixes from the text (LFM_TIE_DIRECT)
+    uint32_t cs_pack;        // bwt_bucket packs buckets greedily into chunks (LFM_CS_PACK=0: cuts at multiples of 1 024)
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -473,10 +474,14 @@ constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 %
 //  bwt_bucket      one workgroup per stream: a counting sort of the rotations
 //                  by their leading kBucketBits bits (byte 0, top bits of byte 1), the
 //                  histogram in LDS; only the values are scattered (the sorters rebuild the 8-byte big-endian keys from the text).
-//                  The stream's slot range is cut at bucket ends into chunks
-//                  of < 2 kChunk rotations (a cut after the bucket that holds
-//                  each multiple of kChunk; a bucket larger than kChunk is a
-//                  chunk of its own).
+//                  The stream's slot range is cut at bucket ends into chunks:
+//                  candidate cuts after each bucket that holds a multiple of
+//                  a grain (256 for the default blocks) and around every
+//                  bucket larger than kSmallCap, then one wave packs whole
+//                  buckets greedily into chunks of at most kSmallCap (a bucket
+//                  larger than that is a chunk of its own).  The sorters'
+//                  capacity is what they cost: packing fills them to ~0.8
+//                  (cuts at multiples of 1 024 alone: 0.67).
 //  bwt_chunk_sort  one workgroup per chunk: the chunk's rotations sorted by the
 //                  whole key in LDS (buckets are ordered by the key's top bits,
 //                  so sorting a run of whole buckets sorts each bucket), and
@@ -492,22 +497,21 @@ constexpr uint32_t kBucketBits = 14;               // default: 64 KiB histogram,
 constexpr uint32_t kMinBucketBits = 13, kMaxBucketBits = 15;
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
-constexpr uint32_t kChunk = 1024;
 constexpr int kCsThreads = 512, kCsItems = 4;      // chunks up to 2 048 (every multi-bucket chunk); 512 x 4 measured
                                                    // 10 % faster than 256 x 8
 constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
 constexpr uint32_t kSmallCap = kCsThreads * kCsItems, kBigCap = kBigThreads * kBigItems;
-constexpr uint32_t kMaxCuts = 1024;                // >= 3 * cap / kChunk + 2
+constexpr uint32_t kMaxCuts = 2048;                // candidate cuts per stream (the grain grows with the cap to fit)
 
 // chunk lists: [3] <= kTinyCap, [0] <= kSmallCap, [1] <= kBigCap, [2] larger
-// (rocPRIM segmented sort)
-constexpr uint32_t kTinyCap = 1024;  // half-size sorter: the ~40 % of chunks at most
-                                     // this long would pad a kSmallCap sort to twice their size
+// (rocPRIM segmented sort).  rocPRIM's block merge sort takes power-of-two
+// shapes only, so no 3 072 sorter for the 2 049 .. 3 072 buckets.
+constexpr uint32_t kTinyCap = 1024;  // half-size sorter
+constexpr int kChunkClasses = 4;
 struct ChunkLists {
-    uint32_t* b[4];
-    uint32_t* e[4];
-    uint32_t* cnt;   // counters of classes 0..2
-    uint32_t* cnt3;  // counter of class 3
+    uint32_t* b[kChunkClasses];
+    uint32_t* e[kChunkClasses];
+    uint32_t* cnt[kChunkClasses];  // chunk counter of each class
 };
 
 // A tile of the text for the bucket pass: T[i0 - 1 .. i0 + m + 8) cyclically
@@ -562,7 +566,8 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     __shared__ uint8_t tile[kBktTile + 16];
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
-    __shared__ uint32_t ccount[4], cbase[4];
+    __shared__ uint32_t ccount[kChunkClasses], cbase[kChunkClasses];
+    __shared__ uint32_t s_nch;
     __shared__ uint32_t sinuse[8];  // bytes present in the RLE1 text (the stream's inUse map)
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
@@ -573,7 +578,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     // see up to 15 bytes past n, which must read as "not tied"
     if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
     for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
-    if (t < 4) ccount[t] = 0;
+    if (t < (uint32_t)kChunkClasses) ccount[t] = 0;
     if (t < 8) sinuse[t] = 0;
     // histogram of the BITS-bit bucket
     BktPart nx = bucket_fetch(T, n, 0);
@@ -604,18 +609,27 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     uint32_t psum = 0;
     for (uint32_t w = 0; w < wave; ++w) psum += wsum[w];
     const uint32_t my0 = psum + isum - sum;
-    // cut positions of this thread's buckets (ascending): after a bucket that
-    // holds a multiple of kChunk, and around a bucket larger than kChunk
+    // candidate cuts of this thread's buckets (ascending): after a bucket that
+    // holds a multiple of the grain G, and around a bucket larger than
+    // kSmallCap.  G doubles until every candidate of a full stream fits
+    // kMaxCuts (cap / G grain cuts + 2 per bucket over kSmallCap + the end).
+    uint32_t G = B.cs_pack ? 256u : 1024u;
+    const uint32_t big = B.cs_pack ? kSmallCap : 1024u;  // a bucket over this is a chunk of its own
+    while (B.cap / G + 2 * (B.cap / (big + 1)) + 2 > kMaxCuts) G *= 2;
+    if (G > kBigCap - kSmallCap) {  // a multi-bucket chunk could pass kBigCap (no such block: cap <= 1.2 M)
+        if (t == 0) atomicOr(&B.flags[s], kFlagHost);
+        return;
+    }
     auto cuts_of = [&](auto&& emit) {
         uint32_t off = my0;
         for (uint32_t q = 0; q < per; ++q) {
             const uint32_t c = hist[t * per + q];
             if (c) {
                 const uint32_t e = off + c;
-                if (c > kChunk) {
+                if (c > big) {
                     if (off) emit(off);
                     emit(e);
-                } else if ((e - 1) / kChunk >= (off + kChunk - 1) / kChunk && e - 1 >= kChunk) {
+                } else if ((e - 1) / G >= (off + G - 1) / G && e - 1 >= G) {
                     emit(e);
                 }
             }
@@ -636,13 +650,15 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         if (w < wave) pcut += wcut[w];
         tcut += wcut[w];
     }
+    if (tcut + 1 > kMaxCuts) {  // cannot happen with the grain above; the host library takes the stream
+        if (t == 0) atomicOr(&B.flags[s], kFlagHost);
+        return;
+    }
     {
         uint32_t at = pcut + icut - ncut;
-        cuts_of([&](uint32_t p) {
-            if (at < kMaxCuts) cuts[at] = p;
-            ++at;
-        });
+        cuts_of([&](uint32_t p) { cuts[at++] = p; });
     }
+    if (t == 0) cuts[tcut] = n;  // the last candidate
     if (t < 8) B.inuse[s * 8 + t] = sinuse[t];  // (written after the scan's barrier)
     // bucket starts for the scatter
     {
@@ -654,23 +670,59 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         }
     }
     __syncthreads();
-    // chunks = runs between consecutive cuts (the last ends at n)
-    const uint32_t nch = min(tcut, kMaxCuts - 1) + 1;
-    uint32_t cb = 0, ce = 0, cls = 0, slot = 0;
-    if (t < nch) {
-        cb = t ? cuts[t - 1] : 0u;
-        ce = t + 1 < nch ? cuts[t] : n;
-        const uint32_t m = ce > cb ? ce - cb : 0u;
-        cls = m <= kTinyCap ? 3u : (m <= kSmallCap ? 0u : (m <= kBigCap ? 1u : 2u));
-        if (m) slot = atomicAdd(&ccount[cls], 1u);
-        else cb = ce;
+    // greedy packing (wave 0): from the chunk start s0, the farthest candidate
+    // within s0 + kSmallCap (a ballot over 64 candidates at a time), else the
+    // next one (a bucket over kSmallCap, or a bucket that ends past the limit:
+    // at most G + kSmallCap).  Chunk ends overwrite the candidates in place
+    // (chunk k ends at a candidate of index >= k, read before the write).
+    if (wave == 0) {
+        const uint32_t tc = tcut + 1;
+        uint32_t s0 = 0, i = 0, nout = 0;
+        while (s0 < n) {
+            while (cuts[i] <= s0) ++i;  // duplicates (a bucket end that is also a big bucket's start)
+            const uint32_t lim = B.cs_pack ? s0 + kSmallCap : s0;  // no packing: every candidate ends a chunk
+            int best = -1;
+            for (uint32_t base = i; base < tc; base += 64) {
+                const uint32_t j = base + lane;
+                const uint64_t mk = __ballot(j < tc && cuts[j] <= lim);
+                if (mk) best = (int)(base + 63u - (uint32_t)__clzll(mk));
+                if (mk != ~0ull) break;
+            }
+            const uint32_t bi = best >= 0 ? (uint32_t)best : i;
+            const uint32_t e = cuts[bi];
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) cuts[nout] = e;
+            ++nout;
+            s0 = e;
+            i = bi + 1;
+        }
+        if (lane == 0) s_nch = nout;
     }
     __syncthreads();
-    if (t < 4) cbase[t] = ccount[t] ? atomicAdd(t < 3 ? &L.cnt[t] : L.cnt3, ccount[t]) : 0u;
+    // classes: [3] tiny, [0] small, [1] big, [2] larger (one bucket)
+    const uint32_t nch = s_nch;
+    uint32_t cb[2] = {0, 0}, ce[2] = {0, 0}, cls[2] = {0, 0}, slot[2] = {0, 0};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t u = t + r * kBucketThreads;  // nch <= kMaxCuts = 2 x threads
+        if (u < nch) {
+            cb[r] = u ? cuts[u - 1] : 0u;
+            ce[r] = cuts[u];
+            const uint32_t m = ce[r] - cb[r];
+            cls[r] = m <= kTinyCap ? 3u : m <= kSmallCap ? 0u : m <= kBigCap ? 1u : 2u;
+            slot[r] = atomicAdd(&ccount[cls[r]], 1u);
+        }
+    }
     __syncthreads();
-    if (t < nch && ce > cb) {
-        L.b[cls][cbase[cls] + slot] = o + cb;
-        L.e[cls][cbase[cls] + slot] = o + ce;
+    if (t < (uint32_t)kChunkClasses) cbase[t] = ccount[t] ? atomicAdd(L.cnt[t], ccount[t]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t u = t + r * kBucketThreads;
+        if (u < nch) {
+            L.b[cls[r]][cbase[cls[r]] + slot[r]] = o + cb[r];
+            L.e[cls[r]][cbase[cls[r]] + slot[r]] = o + ce[r];
+        }
     }
     // scatter of the values only (start | preceding byte << 24): the sorters
     // rebuild the 8-byte keys from the text (rot_key8_fast), which the L2s
@@ -3221,6 +3273,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.nblock_max = 100000u * level - 19u;
     static const uint32_t tie_direct = !(std::getenv("LFM_TIE_DIRECT") && std::atoi(std::getenv("LFM_TIE_DIRECT")) == 0);
     B.tie_direct = tie_direct;
+    static const uint32_t cs_pack = !(std::getenv("LFM_CS_PACK") && std::atoi(std::getenv("LFM_CS_PACK")) == 0);
+    B.cs_pack = cs_pack;
     if (ws_bytes < lfm_hip_bzip2_workspace_bytes(count, raw_cap)) return LFM_HIP_EINVAL;
     const size_t N = (size_t)count * B.cap;
     if (N >= (1ull << 32)) return LFM_HIP_EINVAL;
@@ -3279,13 +3333,16 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
     {
         ChunkLists CL;
-        const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
-        for (int c = 0; c < 4; ++c) {
+        const size_t q = N / kChunkClasses;  // chunk lists in the cl0 / cl1 areas (<= kMaxCuts chunks per stream)
+        for (int c = 0; c < kChunkClasses; ++c) {
             CL.b[c] = B.cl0 + c * q;
             CL.e[c] = B.cl1 + c * q;
         }
-        CL.cnt = d_cnt;
-        CL.cnt3 = d_cnt + 5;
+        // counters: classes 0..2 at [0..2], class 3 at [5]
+        CL.cnt[0] = d_cnt;
+        CL.cnt[1] = d_cnt + 1;
+        CL.cnt[2] = d_cnt + 2;
+        CL.cnt[3] = d_cnt + 5;
         uint32_t nch[6] = {0, 0, 0, 0, 0, 0};
         if (hipMemsetAsync(d_cnt, 0, 32, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
@@ -3333,12 +3390,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             const uint32_t cls_th[3] = {kTinyCap / 8, kSmallCap / 8, kBigCap / 8};
             for (int q = 0; q < 3; ++q) {
                 if (!cls_n[q]) continue;
+                const void* f = fk[q];
                 const dim3 g = cs_grid(cls_n[q], per);
                 const uint32_t* cbq = cls_b[q];
                 const uint32_t* ceq = cls_e[q];
                 uint32_t nq = cls_n[q];
                 void* args[] = {&B, &cbq, &ceq, &nq, &per};
-                if (hipLaunchKernel(fk[q], g, dim3(cls_th[q]), args, 0, st) != hipSuccess) return LFM_HIP_ERUNTIME;
+                if (hipLaunchKernel(f, g, dim3(cls_th[q]), args, 0, st) != hipSuccess) return LFM_HIP_ERUNTIME;
             }
             nch[5] = nch[0] = nch[1] = 0;  // done: only the rocPRIM segmented class below
         }
