@@ -123,7 +123,8 @@ struct Batch {
     uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
     uint32_t* wide_cnt;
     uint32_t tie_direct;     // chunk sorts resolve runs of equal prefixes from the text (LFM_TIE_DIRECT)
-    uint32_t cs_pack;        // bwt_bucket packs buckets greedily into chunks (LFM_CS_PACK=0: cuts at multiples of 1 024)
+    uint32_t cs_pack;        // bwt_bucket packs buckets greedily into chunks of at most this many rotations
+                             // (LFM_CS_PACK: 2048 or 4096; 0 = cuts at multiples of 1 024)
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -613,10 +614,14 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     // holds a multiple of the grain G, and around a bucket larger than
     // kSmallCap.  G doubles until every candidate of a full stream fits
     // kMaxCuts (cap / G grain cuts + 2 per bucket over kSmallCap + the end).
+    // A chunk is at most G + (the largest bucket not on its own) rotations, and
+    // a multi-bucket chunk must stay within kBigCap (the segmented sort of
+    // larger chunks orders single buckets only): buckets over
+    // min(packing limit, kBigCap - G) are chunks of their own.
     uint32_t G = B.cs_pack ? 256u : 1024u;
-    const uint32_t big = B.cs_pack ? kSmallCap : 1024u;  // a bucket over this is a chunk of its own
-    while (B.cap / G + 2 * (B.cap / (big + 1)) + 2 > kMaxCuts) G *= 2;
-    if (G > kBigCap - kSmallCap) {  // a multi-bucket chunk could pass kBigCap (no such block: cap <= 1.2 M)
+    while (B.cap / G + 2 * (B.cap / (kSmallCap / 2 + 1)) + 2 > kMaxCuts) G *= 2;
+    const uint32_t big = min(B.cs_pack ? B.cs_pack : 1024u, kBigCap - min(G, kBigCap));
+    if (big < G) {  // no such block (cap <= 1.2 M): the host library takes the stream
         if (t == 0) atomicOr(&B.flags[s], kFlagHost);
         return;
     }
@@ -680,7 +685,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         uint32_t s0 = 0, i = 0, nout = 0;
         while (s0 < n) {
             while (cuts[i] <= s0) ++i;  // duplicates (a bucket end that is also a big bucket's start)
-            const uint32_t lim = B.cs_pack ? s0 + kSmallCap : s0;  // no packing: every candidate ends a chunk
+            const uint32_t lim = s0 + B.cs_pack;  // no packing (0): every candidate ends a chunk
             int best = -1;
             for (uint32_t base = i; base < tc; base += 64) {
                 const uint32_t j = base + lane;
@@ -2990,7 +2995,9 @@ __global__ __launch_bounds__(kEmitThreads) void emit_stream(Batch B)
         __syncthreads();
         const uint32_t nfull = (uint32_t)(((bitpos & 31) + rbits) >> 5);
         uint32_t* dst = words + (bitpos >> 5);
-        for (uint32_t i = t; i < nfull; i += kEmitThreads) dst[i] = obuf[i];
+        // non-temporal: the stream words are read once more (compaction), and
+        // dirty lines left in the caches slow the next encode's predictor
+        for (uint32_t i = t; i < nfull; i += kEmitThreads) __builtin_nontemporal_store(obuf[i], &dst[i]);
         const uint32_t cv = obuf[nfull];
         __syncthreads();
         for (uint32_t i = 1 + t; i <= nfull; i += kEmitThreads) obuf[i] = 0;
@@ -3041,7 +3048,7 @@ __global__ __launch_bounds__(256) void compact_streams(Batch B, const uint64_t* 
     for (uint64_t a = a0 + t; a < a1; a += 256) {
         const uint64_t w = j0 + (a - a0);
         const uint32_t x = r ? (words[w] << sh) | (words[w + 1] >> (32 - sh)) : words[w];
-        p32[a] = __builtin_bswap32(x);
+        __builtin_nontemporal_store(__builtin_bswap32(x), &p32[a]);  // read next by the SDMA copy
     }
 }
 
@@ -3273,7 +3280,11 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.nblock_max = 100000u * level - 19u;
     static const uint32_t tie_direct = !(std::getenv("LFM_TIE_DIRECT") && std::atoi(std::getenv("LFM_TIE_DIRECT")) == 0);
     B.tie_direct = tie_direct;
-    static const uint32_t cs_pack = !(std::getenv("LFM_CS_PACK") && std::atoi(std::getenv("LFM_CS_PACK")) == 0);
+    static const uint32_t cs_pack = [] {
+        const char* e = std::getenv("LFM_CS_PACK");
+        const int v = e ? std::atoi(e) : (int)kSmallCap;
+        return v == 0 || v == (int)kSmallCap || v == (int)kBigCap ? (uint32_t)v : kSmallCap;
+    }();
     B.cs_pack = cs_pack;
     if (ws_bytes < lfm_hip_bzip2_workspace_bytes(count, raw_cap)) return LFM_HIP_EINVAL;
     const size_t N = (size_t)count * B.cap;

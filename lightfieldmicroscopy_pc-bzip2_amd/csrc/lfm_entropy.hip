@@ -87,6 +87,9 @@ __global__ __launch_bounds__(256) void ent_count(Jobs J, uint32_t* __restrict__ 
         if (zeros) atomicAdd(&h[0], zeros);
     }
     __syncthreads();
+    // non-temporal stores here, in ent_scan and ent_scatter: the selection
+    // runs right before the predictor, which streams 1 GiB and would first
+    // write back any dirty lines these leave in the caches
     cnt[((size_t)job * kSegMax + blockIdx.x) * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
