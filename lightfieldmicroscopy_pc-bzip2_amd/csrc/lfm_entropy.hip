@@ -87,9 +87,9 @@ __global__ __launch_bounds__(256) void ent_count(Jobs J, uint32_t* __restrict__ 
         if (zeros) atomicAdd(&h[0], zeros);
     }
     __syncthreads();
-    // non-temporal stores here, in ent_scan and ent_scatter: the selection
-    // runs right before the predictor, which streams 1 GiB and would first
-    // write back any dirty lines these leave in the caches
+    // (plain stores: non-temporal ones here and in ent_scan gave no measurable
+    // gain, and in ent_scatter's byte scatter they doubled the selection time;
+    // profiles/r03_ab_nt_stores.txt)
     cnt[((size_t)job * kSegMax + blockIdx.x) * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
