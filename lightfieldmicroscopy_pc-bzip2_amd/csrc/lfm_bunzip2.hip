@@ -205,6 +205,64 @@ struct WaveBits {
     __device__ __forceinline__ bool over() const { return 32 * (wi - 2) + off > total; }
 };
 
+// The symbol loop's bit reader in vector registers (bzd_huff<LB, true>):
+// every lane holds the same window, so the lookup is an LDS broadcast read,
+// the decode arithmetic is VALU -- four SIMDs per CU -- and only loop control
+// stays on the CU's one scalar unit, which the ~16 resident streams share
+// (PMC: the scalar unit ~53 % busy with ~21 SALU instructions per symbol in
+// the wave-uniform reader).  Refills read the vector window by ds_bpermute.
+struct LaneBits {
+    const uint32_t* w;
+    uint32_t nw, base, vq, vn, wi, off, total;
+    uint64_t win;
+    __device__ __forceinline__ uint32_t raw(uint32_t i) const { return w[min(i, nw - 1)]; }
+    __device__ __forceinline__ uint32_t fix(uint32_t v, uint32_t i) const { return i < nw ? __builtin_bswap32(v) : 0u; }
+    __device__ __forceinline__ void from(const WaveBits& b)
+    {
+        // the copies go through a lane shuffle so the compiler keeps the
+        // state in vector registers (a shuffle's result is divergent to it)
+        w = b.w;
+        nw = b.nw;
+        base = (uint32_t)__shfl((int)b.base, 0);
+        vq = b.vq;
+        vn = b.vn;
+        wi = (uint32_t)__shfl((int)b.wi, 0);
+        off = (uint32_t)__shfl((int)b.off, 0);
+        total = b.total;
+        win = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(b.win >> 32), 0) << 32) |
+              (uint32_t)__shfl((int)(uint32_t)b.win, 0);
+    }
+    __device__ __forceinline__ void to(WaveBits& b) const
+    {
+        auto U = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+        b.base = U(base);
+        b.vq = vq;
+        b.vn = vn;
+        b.wi = U(wi);
+        b.off = U(off);
+        b.win = ((uint64_t)U((uint32_t)(win >> 32)) << 32) | U((uint32_t)win);
+    }
+    __device__ __forceinline__ uint32_t next()
+    {
+        if (wi - base == 64) {
+            base += 64;
+            vq = fix(vn, base + threadIdx.x);
+            vn = raw(base + 64 + threadIdx.x);
+        }
+        return (uint32_t)__shfl((int)vq, (int)(wi++ - base));
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t nb) const { return (uint32_t)((win << off) >> (64 - nb)); }
+    __device__ __forceinline__ void skip(uint32_t nb)
+    {
+        off += nb;
+        if (off >= 32) {
+            off -= 32;
+            win = (win << 32) | next();
+        }
+    }
+    __device__ __forceinline__ bool over() const { return 32 * (wi - 2) + off > total; }
+};
+
 // inclusive wave sum by DPP row shifts and row broadcasts (no LDS round
 // trips; the lanes a step has no source for add 0)
 template <int CTRL, int ROWS>
@@ -223,7 +281,7 @@ __device__ __forceinline__ uint32_t wave_sum_incl(uint32_t x)
     return x;
 }
 
-template <int LB>
+template <int LB, bool VB>
 __global__ __launch_bounds__(64) void bzd_huff(Dec D)
 {
     __shared__ uint16_t lut[kMaxGroups << LB];
@@ -361,8 +419,10 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         uint32_t rs = 0;       // digits of a run still open at the end of the previous group
         uint32_t g = 0;
         bool eob = false;
+        LaneBits lb;
+        if constexpr (VB) lb.from(br);
         while (!eob) {
-            if (g >= nSel || br.over()) { flag = kHost; break; }
+            if (g >= nSel || (VB ? U((uint32_t)lb.over()) != 0 : br.over())) { flag = kHost; break; }
             const uint32_t tb = ((U(sel[g >> 3]) >> (4 * (g & 7))) & 15u) << LB;
             ++g;
             // 1. Huffman: symbol k of the group into lane k
@@ -395,19 +455,61 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             auto put = [](uint32_t& v, uint32_t sym, uint32_t G) {
                 asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(sym), "s"(G) : "m0");
             };
+            // the same decode with the reader in vector registers (VB): the
+            // symbol is a VGPR, equal in all lanes; a bad code marks the lane
+            bool vbad = false;
+            auto decode1v = [&]() -> uint32_t {
+                const uint32_t e = lut[tb + lb.peek(LB)];
+                uint32_t len = e >> 9;
+                uint32_t sym = e & 511u;
+                if (len == 0) {
+                    const uint32_t t = tb >> LB;
+                    uint32_t zn = LB + 1;
+                    int32_t zvec = (int32_t)lb.peek(zn);
+                    while (zn <= kMaxLen && zvec > slimit[t][zn]) {
+                        ++zn;
+                        zvec = (int32_t)lb.peek(zn);
+                    }
+                    const int idx = zvec - sbase[t][min(zn, (uint32_t)kMaxLen)];
+                    if (zn > kMaxLen || idx < 0 || idx >= alphaSize) {
+                        vbad = true;
+                        zn = 1;
+                        sym = EOB;
+                    } else {
+                        sym = sperm[t][idx];
+                    }
+                    len = zn;
+                }
+                lb.skip(len);
+                return sym;
+            };
             uint32_t symv = 0, G = 0;
             if (g < nSel) {  // not the last group: 50 symbols, none of them EOB (libbzip2 writes
                              // one selector per group, EOB in the last; anything else -> host)
-                for (G = 0; G < 50; ++G) put(symv, decode1(), G);
+                if constexpr (VB) {
+                    for (G = 0; G < 50; ++G) {
+                        const uint32_t sym = decode1v();
+                        symv = lane == G ? sym : symv;
+                    }
+                } else {
+                    for (G = 0; G < 50; ++G) put(symv, decode1(), G);
+                }
                 if (__ballot(lane < 50 && symv == EOB)) flag = kHost;
             } else {
                 do {
-                    const uint32_t sym = decode1();
-                    put(symv, sym, G);
+                    uint32_t sym;
+                    if constexpr (VB) {
+                        sym = U(decode1v());
+                        symv = lane == G ? sym : symv;
+                    } else {
+                        sym = decode1();
+                        put(symv, sym, G);
+                    }
                     ++G;
                     eob = sym == EOB;
                 } while (G < 50 && !eob);
             }
+            if (VB && __ballot(vbad)) flag = kHost;
             if (flag) break;
             // 2. runs and counts over the lanes
             const bool valid = lane < G;
@@ -467,6 +569,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             rs = (uint32_t)__builtin_amdgcn_readlane((int)(isrun ? j + 1u : 0u), (int)(G - 1));
         }
         if (flag) break;
+        if constexpr (VB) lb.to(br);
         if (origPtr >= nblock || nblock == 0) { flag = kHost; break; }
         // end of stream: exactly one block
         const uint32_t e1 = br.get(24), e2 = br.get(24);
@@ -990,9 +1093,18 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
         const int b = e ? atoi(e) : 8;
         return b == 9 || b == 10 ? b : 8;
     }();
-    if (lut_bits == 10) hipLaunchKernelGGL(bzd_huff<10>, dim3(count), dim3(64), sel_lds, st, D);
-    else if (lut_bits == 9) hipLaunchKernelGGL(bzd_huff<9>, dim3(count), dim3(64), sel_lds, st, D);
-    else hipLaunchKernelGGL(bzd_huff<8>, dim3(count), dim3(64), sel_lds, st, D);
+    // the symbol loop's bit reader in vector registers (LFM_BZD_VALU=0: wave-uniform scalar reader)
+    static const bool valu = !(getenv("LFM_BZD_VALU") && atoi(getenv("LFM_BZD_VALU")) == 0);
+    if (lut_bits == 10) {
+        if (valu) hipLaunchKernelGGL((bzd_huff<10, true>), dim3(count), dim3(64), sel_lds, st, D);
+        else hipLaunchKernelGGL((bzd_huff<10, false>), dim3(count), dim3(64), sel_lds, st, D);
+    } else if (lut_bits == 9) {
+        if (valu) hipLaunchKernelGGL((bzd_huff<9, true>), dim3(count), dim3(64), sel_lds, st, D);
+        else hipLaunchKernelGGL((bzd_huff<9, false>), dim3(count), dim3(64), sel_lds, st, D);
+    } else {
+        if (valu) hipLaunchKernelGGL((bzd_huff<8, true>), dim3(count), dim3(64), sel_lds, st, D);
+        else hipLaunchKernelGGL((bzd_huff<8, false>), dim3(count), dim3(64), sel_lds, st, D);
+    }
     // LF mapping: LFM_TT_THREADS (256 / 512 / 1024 positions per tile) for A/B runs
     static const int tt_nt = [] {
         const char* e = getenv("LFM_TT_THREADS");

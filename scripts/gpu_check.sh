@@ -18,9 +18,9 @@ step() {  # name timeout cmd...
     return $rc
 }
 rocm-smi --showproductname > "$OUT/rocm_smi.log" 2>&1 || true
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
-step smoke 300 python __graft_entry__.py smoke
-step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup ${BENCH_WARMUP:-5}
+[ "${TESTS:-1}" = "1" ] && step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
+[ "${TESTS:-1}" = "1" ] && step smoke 300 python __graft_entry__.py smoke
+[ "${BENCH:-1}" = "1" ] && step bench 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup ${BENCH_WARMUP:-5}
 if [ "${PROFILE:-1}" = "1" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-host-input
 fi
