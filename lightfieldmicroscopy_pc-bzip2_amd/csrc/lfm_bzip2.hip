@@ -122,9 +122,7 @@ struct Batch {
     uint32_t* out_bytes;
     uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
     uint32_t* wide_cnt;
-    uint32_t tie_direct;     // chunk sorts resolve runs of equal prefixes from the text (LFM_TIE_DIRECT)
-    uint32_t cs_pack;        // bwt_bucket packs buckets greedily into chunks of at most this many rotations
-                             // (LFM_CS_PACK: 2048 or 4096; 0 = cuts at multiples of 1 024)
+    uint32_t tie_direct;     // tie_runs_direct resolves short runs of equal prefixes from the text (LFM_TIE_DIRECT)
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -475,14 +473,10 @@ constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 %
 //  bwt_bucket      one workgroup per stream: a counting sort of the rotations
 //                  by their leading kBucketBits bits (byte 0, top bits of byte 1), the
 //                  histogram in LDS; only the values are scattered (the sorters rebuild the 8-byte big-endian keys from the text).
-//                  The stream's slot range is cut at bucket ends into chunks:
-//                  candidate cuts after each bucket that holds a multiple of
-//                  a grain (256 for the default blocks) and around every
-//                  bucket larger than kSmallCap, then one wave packs whole
-//                  buckets greedily into chunks of at most kSmallCap (a bucket
-//                  larger than that is a chunk of its own).  The sorters'
-//                  capacity is what they cost: packing fills them to ~0.8
-//                  (cuts at multiples of 1 024 alone: 0.67).
+//                  The stream's slot range is cut at bucket ends into chunks
+//                  of < 2 kChunk rotations (a cut after the bucket that holds
+//                  each multiple of kChunk; a bucket larger than kChunk is a
+//                  chunk of its own).
 //  bwt_chunk_sort  one workgroup per chunk: the chunk's rotations sorted by the
 //                  whole key in LDS (buckets are ordered by the key's top bits,
 //                  so sorting a run of whole buckets sorts each bucket), and
@@ -498,21 +492,22 @@ constexpr uint32_t kBucketBits = 14;               // default: 64 KiB histogram,
 constexpr uint32_t kMinBucketBits = 13, kMaxBucketBits = 15;
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
+constexpr uint32_t kChunk = 1024;
 constexpr int kCsThreads = 512, kCsItems = 4;      // chunks up to 2 048 (every multi-bucket chunk); 512 x 4 measured
                                                    // 10 % faster than 256 x 8
 constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
 constexpr uint32_t kSmallCap = kCsThreads * kCsItems, kBigCap = kBigThreads * kBigItems;
-constexpr uint32_t kMaxCuts = 2048;                // candidate cuts per stream (the grain grows with the cap to fit)
+constexpr uint32_t kMaxCuts = 1024;                // >= 3 * cap / kChunk + 2
 
 // chunk lists: [3] <= kTinyCap, [0] <= kSmallCap, [1] <= kBigCap, [2] larger
-// (rocPRIM segmented sort).  rocPRIM's block merge sort takes power-of-two
-// shapes only, so no 3 072 sorter for the 2 049 .. 3 072 buckets.
-constexpr uint32_t kTinyCap = 1024;  // half-size sorter
-constexpr int kChunkClasses = 4;
+// (rocPRIM segmented sort)
+constexpr uint32_t kTinyCap = 1024;  // half-size sorter: the ~40 % of chunks at most
+                                     // this long would pad a kSmallCap sort to twice their size
 struct ChunkLists {
-    uint32_t* b[kChunkClasses];
-    uint32_t* e[kChunkClasses];
-    uint32_t* cnt[kChunkClasses];  // chunk counter of each class
+    uint32_t* b[4];
+    uint32_t* e[4];
+    uint32_t* cnt;   // counters of classes 0..2
+    uint32_t* cnt3;  // counter of class 3
 };
 
 // A tile of the text for the bucket pass: T[i0 - 1 .. i0 + m + 8) cyclically
@@ -567,8 +562,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     __shared__ uint8_t tile[kBktTile + 16];
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
-    __shared__ uint32_t ccount[kChunkClasses], cbase[kChunkClasses];
-    __shared__ uint32_t s_nch;
+    __shared__ uint32_t ccount[4], cbase[4];
     __shared__ uint32_t sinuse[8];  // bytes present in the RLE1 text (the stream's inUse map)
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
@@ -579,7 +573,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     // see up to 15 bytes past n, which must read as "not tied"
     if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
     for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
-    if (t < (uint32_t)kChunkClasses) ccount[t] = 0;
+    if (t < 4) ccount[t] = 0;
     if (t < 8) sinuse[t] = 0;
     // histogram of the BITS-bit bucket
     BktPart nx = bucket_fetch(T, n, 0);
@@ -610,31 +604,18 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     uint32_t psum = 0;
     for (uint32_t w = 0; w < wave; ++w) psum += wsum[w];
     const uint32_t my0 = psum + isum - sum;
-    // candidate cuts of this thread's buckets (ascending): after a bucket that
-    // holds a multiple of the grain G, and around a bucket larger than
-    // kSmallCap.  G doubles until every candidate of a full stream fits
-    // kMaxCuts (cap / G grain cuts + 2 per bucket over kSmallCap + the end).
-    // A chunk is at most G + (the largest bucket not on its own) rotations, and
-    // a multi-bucket chunk must stay within kBigCap (the segmented sort of
-    // larger chunks orders single buckets only): buckets over
-    // min(packing limit, kBigCap - G) are chunks of their own.
-    uint32_t G = B.cs_pack ? 256u : 1024u;
-    while (B.cap / G + 2 * (B.cap / (kSmallCap / 2 + 1)) + 2 > kMaxCuts) G *= 2;
-    const uint32_t big = min(B.cs_pack ? B.cs_pack : 1024u, kBigCap - min(G, kBigCap));
-    if (big < G) {  // no such block (cap <= 1.2 M): the host library takes the stream
-        if (t == 0) atomicOr(&B.flags[s], kFlagHost);
-        return;
-    }
+    // cut positions of this thread's buckets (ascending): after a bucket that
+    // holds a multiple of kChunk, and around a bucket larger than kChunk
     auto cuts_of = [&](auto&& emit) {
         uint32_t off = my0;
         for (uint32_t q = 0; q < per; ++q) {
             const uint32_t c = hist[t * per + q];
             if (c) {
                 const uint32_t e = off + c;
-                if (c > big) {
+                if (c > kChunk) {
                     if (off) emit(off);
                     emit(e);
-                } else if ((e - 1) / G >= (off + G - 1) / G && e - 1 >= G) {
+                } else if ((e - 1) / kChunk >= (off + kChunk - 1) / kChunk && e - 1 >= kChunk) {
                     emit(e);
                 }
             }
@@ -655,15 +636,13 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         if (w < wave) pcut += wcut[w];
         tcut += wcut[w];
     }
-    if (tcut + 1 > kMaxCuts) {  // cannot happen with the grain above; the host library takes the stream
-        if (t == 0) atomicOr(&B.flags[s], kFlagHost);
-        return;
-    }
     {
         uint32_t at = pcut + icut - ncut;
-        cuts_of([&](uint32_t p) { cuts[at++] = p; });
+        cuts_of([&](uint32_t p) {
+            if (at < kMaxCuts) cuts[at] = p;
+            ++at;
+        });
     }
-    if (t == 0) cuts[tcut] = n;  // the last candidate
     if (t < 8) B.inuse[s * 8 + t] = sinuse[t];  // (written after the scan's barrier)
     // bucket starts for the scatter
     {
@@ -675,59 +654,23 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         }
     }
     __syncthreads();
-    // greedy packing (wave 0): from the chunk start s0, the farthest candidate
-    // within s0 + kSmallCap (a ballot over 64 candidates at a time), else the
-    // next one (a bucket over kSmallCap, or a bucket that ends past the limit:
-    // at most G + kSmallCap).  Chunk ends overwrite the candidates in place
-    // (chunk k ends at a candidate of index >= k, read before the write).
-    if (wave == 0) {
-        const uint32_t tc = tcut + 1;
-        uint32_t s0 = 0, i = 0, nout = 0;
-        while (s0 < n) {
-            while (cuts[i] <= s0) ++i;  // duplicates (a bucket end that is also a big bucket's start)
-            const uint32_t lim = s0 + B.cs_pack;  // no packing (0): every candidate ends a chunk
-            int best = -1;
-            for (uint32_t base = i; base < tc; base += 64) {
-                const uint32_t j = base + lane;
-                const uint64_t mk = __ballot(j < tc && cuts[j] <= lim);
-                if (mk) best = (int)(base + 63u - (uint32_t)__clzll(mk));
-                if (mk != ~0ull) break;
-            }
-            const uint32_t bi = best >= 0 ? (uint32_t)best : i;
-            const uint32_t e = cuts[bi];
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) cuts[nout] = e;
-            ++nout;
-            s0 = e;
-            i = bi + 1;
-        }
-        if (lane == 0) s_nch = nout;
+    // chunks = runs between consecutive cuts (the last ends at n)
+    const uint32_t nch = min(tcut, kMaxCuts - 1) + 1;
+    uint32_t cb = 0, ce = 0, cls = 0, slot = 0;
+    if (t < nch) {
+        cb = t ? cuts[t - 1] : 0u;
+        ce = t + 1 < nch ? cuts[t] : n;
+        const uint32_t m = ce > cb ? ce - cb : 0u;
+        cls = m <= kTinyCap ? 3u : (m <= kSmallCap ? 0u : (m <= kBigCap ? 1u : 2u));
+        if (m) slot = atomicAdd(&ccount[cls], 1u);
+        else cb = ce;
     }
     __syncthreads();
-    // classes: [3] tiny, [0] small, [1] big, [2] larger (one bucket)
-    const uint32_t nch = s_nch;
-    uint32_t cb[2] = {0, 0}, ce[2] = {0, 0}, cls[2] = {0, 0}, slot[2] = {0, 0};
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const uint32_t u = t + r * kBucketThreads;  // nch <= kMaxCuts = 2 x threads
-        if (u < nch) {
-            cb[r] = u ? cuts[u - 1] : 0u;
-            ce[r] = cuts[u];
-            const uint32_t m = ce[r] - cb[r];
-            cls[r] = m <= kTinyCap ? 3u : m <= kSmallCap ? 0u : m <= kBigCap ? 1u : 2u;
-            slot[r] = atomicAdd(&ccount[cls[r]], 1u);
-        }
-    }
+    if (t < 4) cbase[t] = ccount[t] ? atomicAdd(t < 3 ? &L.cnt[t] : L.cnt3, ccount[t]) : 0u;
     __syncthreads();
-    if (t < (uint32_t)kChunkClasses) cbase[t] = ccount[t] ? atomicAdd(L.cnt[t], ccount[t]) : 0u;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        const uint32_t u = t + r * kBucketThreads;
-        if (u < nch) {
-            L.b[cls[r]][cbase[cls[r]] + slot[r]] = o + cb[r];
-            L.e[cls[r]][cbase[cls[r]] + slot[r]] = o + ce[r];
-        }
+    if (t < nch && ce > cb) {
+        L.b[cls][cbase[cls] + slot] = o + cb;
+        L.e[cls][cbase[cls] + slot] = o + ce;
     }
     // scatter of the values only (start | preceding byte << 24): the sorters
     // rebuild the 8-byte keys from the text (rot_key8_fast), which the L2s
@@ -779,13 +722,13 @@ __global__ __launch_bounds__(256) void bwt_chunk_keys(Batch B, const uint32_t* _
     for (uint32_t j = cb + threadIdx.x; j < ce; j += 256) B.keys_a[j] = rot_key8_fast(T, n, B.vals_a[j] & kIdxMask);
 }
 
-// Runs of rotations whose 8-byte prefixes are equal, resolved inside the
-// chunk sort when short: at most kTieRunMax rotations, ordered by insertion
+// Runs of rotations whose 8-byte prefixes are equal, resolved right after the
+// chunk sorts when short: at most kTieRunMax rotations, ordered by insertion
 // on their cyclic text from byte kKeyBytes on, kTieCmpBytes at most per
 // comparison (bzip2 orders the rotations of the block lexicographically).  A
-// longer run, or one with a comparison still equal after kTieCmpBytes, keeps
-// its flags for the device-wide tie rounds, whose result does not depend on
-// the order the run is left in.
+// longer run, or one with a comparison still equal after kTieCmpBytes, is left
+// to the device-wide tie rounds, whose result does not depend on the order
+// the run is left in.
 constexpr uint32_t kTieRunMax = 32;
 constexpr uint32_t kTieCmpBytes = 64;
 
@@ -803,30 +746,50 @@ __device__ __forceinline__ int tie_cmp(const uint8_t* __restrict__ T, uint32_t n
     return 0;
 }
 
-// the run of prefix K starting at sorted position pos of a chunk (values sv,
-// still-tied flags fl in LDS, m positions): sort it and clear its flags
-__device__ void tie_run_sort(uint32_t* sv, uint8_t* fl, uint32_t pos, uint32_t m, uint64_t K,
-                             const uint8_t* __restrict__ T, uint32_t n)
+// One thread per run of the tied list (the still-tied slots after the chunk
+// sorts, in slot order; a run is consecutive slots of one prefix): the run's
+// values in sa sorted in place.  The slots keep their flags, so tie rounds
+// that still run (some run here too long or undecided: counted in *unres)
+// re-sort the resolved runs to the same order; with *unres == 0 the host
+// skips them.  A separate launch keeps the chunk sort's registers (inlined
+// there, this code took it from 37 to 88 VGPRs and 8 to 5 waves per SIMD).
+__global__ __launch_bounds__(256) void tie_runs_direct(Batch B, const uint32_t* __restrict__ cl,
+                                                  const uint32_t* __restrict__ cnt_p, uint32_t* __restrict__ unres)
 {
-    uint32_t e = pos + 1;
-    while (e < m && e - pos <= kTieRunMax && fl[e] && rot_key8_fast(T, n, sv[e] & kIdxMask) == K) ++e;
-    if (e - pos > kTieRunMax) return;
-    for (uint32_t x = pos + 1; x < e; ++x) {
-        const uint32_t vx = sv[x];
-        uint32_t y = x;
-        while (y > pos) {
-            const int c = tie_cmp(T, n, sv[y - 1] & kIdxMask, vx & kIdxMask);
-            if (c == 0) {  // undecided: the run stays flagged (same elements, any order)
-                sv[y] = vx;
-                return;
-            }
-            if (c < 0) break;
-            sv[y] = sv[y - 1];
-            --y;
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < cnt; c += gridDim.x * blockDim.x) {
+        const uint32_t slot = cl[c];
+        const uint32_t s = slot / B.cap, n = B.n[s];
+        const uint8_t* T = B.T + (size_t)s * B.cap;
+        const uint64_t K = rot_key8_fast(T, n, B.sa[slot] & kIdxMask);
+        if (c > 0 && cl[c - 1] == slot - 1 && rot_key8_fast(T, n, B.sa[slot - 1] & kIdxMask) == K) continue;
+        uint32_t g = 1;
+        while (c + g < cnt && g <= kTieRunMax && cl[c + g] == slot + g &&
+               rot_key8_fast(T, n, B.sa[slot + g] & kIdxMask) == K)
+            ++g;
+        if (g > kTieRunMax) {
+            atomicAdd(unres, 1u);
+            continue;
         }
-        sv[y] = vx;
+        uint32_t* sv = B.sa + slot;
+        bool ok = true;
+        for (uint32_t x = 1; x < g && ok; ++x) {
+            const uint32_t vx = sv[x];
+            uint32_t y = x;
+            while (y > 0) {
+                const int cmp = tie_cmp(T, n, sv[y - 1] & kIdxMask, vx & kIdxMask);
+                if (cmp == 0) {  // undecided: the rounds re-sort the run (same elements, any order)
+                    ok = false;
+                    break;
+                }
+                if (cmp < 0) break;
+                sv[y] = sv[y - 1];
+                --y;
+            }
+            sv[y] = vx;
+        }
+        if (!ok) atomicAdd(unres, 1u);
     }
-    for (uint32_t x = pos; x < e; ++x) fl[x] = 0;
 }
 
 // The chunk's keys / values are loaded striped (element q * TH + t: coalesced),
@@ -905,27 +868,10 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
         if constexpr (IPT == 8) *(uint64_t*)&sm.x.fl[t * IPT] = fpack;
         else *(uint32_t*)&sm.x.fl[t * IPT] = (uint32_t)fpack;
     }
-    // runs of equal 8-byte prefixes (~0.02 % of rotations, nearly always
-    // pairs): sorted here by their text from byte 8 on, so the device-wide tie
-    // rounds -- dozens of tiny kernels and host round trips -- mostly find
-    // nothing left.  The thread owning a run's first position sorts it.
-    if (__syncthreads_or(nt != 0)) {
-        if (B.tie_direct) {
-#pragma unroll
-            for (int q = 0; q < IPT; ++q) {
-                const uint32_t pos = t * IPT + q;
-                const uint64_t lo = q ? k[q - 1] : kprev;
-                if (((fpack >> (8 * q)) & 1u) && (pos == 0 || lo != k[q])) tie_run_sort(sm.x.sv, sm.x.fl, pos, m, k[q], T, n);
-            }
-        }
-        __syncthreads();
-        nt = 0;
-    }
+    __syncthreads();
     for (uint32_t j = t; j < m; j += TH) {
-        const uint8_t f = sm.x.fl[j];
         B.sa[cb + j] = sm.x.sv[j];
-        B.uflag[cb + j] = f;
-        nt += f;
+        B.uflag[cb + j] = sm.x.fl[j];
     }
     if (__any(nt)) {
         for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
@@ -3280,12 +3226,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.nblock_max = 100000u * level - 19u;
     static const uint32_t tie_direct = !(std::getenv("LFM_TIE_DIRECT") && std::atoi(std::getenv("LFM_TIE_DIRECT")) == 0);
     B.tie_direct = tie_direct;
-    static const uint32_t cs_pack = [] {
-        const char* e = std::getenv("LFM_CS_PACK");
-        const int v = e ? std::atoi(e) : (int)kSmallCap;
-        return v == 0 || v == (int)kSmallCap || v == (int)kBigCap ? (uint32_t)v : kSmallCap;
-    }();
-    B.cs_pack = cs_pack;
     if (ws_bytes < lfm_hip_bzip2_workspace_bytes(count, raw_cap)) return LFM_HIP_EINVAL;
     const size_t N = (size_t)count * B.cap;
     if (N >= (1ull << 32)) return LFM_HIP_EINVAL;
@@ -3344,16 +3284,13 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
     {
         ChunkLists CL;
-        const size_t q = N / kChunkClasses;  // chunk lists in the cl0 / cl1 areas (<= kMaxCuts chunks per stream)
-        for (int c = 0; c < kChunkClasses; ++c) {
+        const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
+        for (int c = 0; c < 4; ++c) {
             CL.b[c] = B.cl0 + c * q;
             CL.e[c] = B.cl1 + c * q;
         }
-        // counters: classes 0..2 at [0..2], class 3 at [5]
-        CL.cnt[0] = d_cnt;
-        CL.cnt[1] = d_cnt + 1;
-        CL.cnt[2] = d_cnt + 2;
-        CL.cnt[3] = d_cnt + 5;
+        CL.cnt = d_cnt;
+        CL.cnt3 = d_cnt + 5;
         uint32_t nch[6] = {0, 0, 0, 0, 0, 0};
         if (hipMemsetAsync(d_cnt, 0, 32, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
@@ -3452,6 +3389,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (e == hipSuccess) {
         hipLaunchKernelGGL(tie_offsets, dim3(1), dim3(1024), 0, st, B, d_cnt);
         hipLaunchKernelGGL(tie_compact, dim3(count), dim3(256), 0, st, B, B.cl0);
+        if (B.tie_direct) hipLaunchKernelGGL(tie_runs_direct, dim3(1024), dim3(256), 0, st, B, B.cl0, d_cnt, d_cnt + 7);
         if (!ok()) return LFM_HIP_ERUNTIME;
     }
     uint32_t covered = kKeyBytes;
@@ -3459,19 +3397,24 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     // text rounds over the tied list (group keys: u64 per entry in the rank
     // area, group index / bounds in the mtfv area -- both free here)
     bool none_left = false;  // a count read 0 and no kernel ran since: skip the later reads
-    uint32_t first_ties = 0;  // rotations still tied after the chunk sorts (LFM_BZ2_STATS)
+    uint32_t first_ties = 0, left_runs = 0;  // tied slots after the chunk sorts, runs tie_runs_direct left (LFM_BZ2_STATS)
     {
         uint64_t* gk = (uint64_t*)B.rank;
         uint32_t* bnd = (uint32_t*)B.mtfv;
         for (int r = 0; r < kTextRounds && e == hipSuccess; ++r) {
-            uint32_t cnt = 0;
-            if (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            // counters: [0] tied slots, [7] runs tie_runs_direct left (read with the first round's count)
+            uint32_t c8[8] = {};
+            if (hipMemcpyAsync(c8, d_cnt, r == 0 ? 32 : 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {
                 e = hipErrorUnknown;
                 break;
             }
-            if (r == 0) first_ties = cnt;
-            if (cnt == 0) {  // nothing tied (the usual case once the chunk sorts resolve their runs)
+            const uint32_t cnt = c8[0];
+            if (r == 0) {
+                first_ties = cnt;
+                left_runs = c8[7];
+            }
+            if (cnt == 0 || (r == 0 && B.tie_direct && c8[7] == 0)) {  // nothing tied, or tie_runs_direct sorted every run
                 none_left = true;
                 break;
             }
@@ -3630,7 +3573,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         uint32_t c[8] = {};
         if (hipMemcpyAsync(c, d_cnt, 32, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
             std::fprintf(stderr, "lfm_bzip2 stats: %u streams, %u with u64 Huffman heaps, Huffman retries %u, "
-                         "tied after the chunk sorts %u\n", count, c[3], c[4], first_ties);
+                         "tied after the chunk sorts %u, runs left to the tie rounds %u\n", count, c[3], c[4], first_ties,
+                         left_runs);
     }
     std::vector<uint32_t> nbytes(count);
     if (hipMemcpyAsync(nbytes.data(), B.out_bytes, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
