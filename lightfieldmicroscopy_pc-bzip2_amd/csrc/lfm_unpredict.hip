@@ -21,7 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 #include "lfm_cases.h"
 #include "lfm_hip.h"
 
@@ -69,7 +71,11 @@ struct UnFrames {
     uint16_t* out;         // nz decoded frames
     int W, H, T, nz, z0, video;
     int first, step;       // this launch decodes local frames first, first + step, ...
+    // diagnostics (LFM_UNPREDICT_TRACE): per band5 workgroup, kTraceSlots
+    // 100 MHz timestamps (band start, then before / after each round's wait)
+    unsigned long long* trace;
 };
+constexpr int kTraceSlots = 512;
 
 template <int FAM, int K>
 __global__ __launch_bounds__(64) void unpredict_band(UnFrames p)
@@ -410,8 +416,14 @@ constexpr int kHand = 128;
 constexpr int kSync = 32;
 
 // XCU (cross-CU, band5 below): every band is its own workgroup, so `pos` lives
-// in global memory and the progress words, their fences and the hand-over
-// loads of the band above's rows use agent scope instead of workgroup scope.
+// in global memory and the progress words and the hand-over loads of the band
+// above's rows use agent scope instead of workgroup scope.  The hand-over is
+// write-through instead of fenced: every output store is a 16-byte `sc1`
+// buffer store, drained (`s_waitcnt vmcnt(0)`) before the progress word (an
+// `sc1` store) is written, and every load of another band's rows is an `sc1`
+// load to registers, so neither side needs an agent-scope fence (a release
+// fence is `buffer_wbl2 sc1`, a write-back of the XCD's whole L2, an acquire
+// `buffer_inv sc1`; band5 issued both every 32 steps of every band).
 template <int FAM, int K, bool TEMP, bool XCU = false>
 __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv, uint16_t* lds, int ring_off,
                                       int hand_off, int* pos)
@@ -421,27 +433,30 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
     const size_t fs = (size_t)p.W * p.H;
     const uint16_t* sym = p.sym + fz * fs;
     uint16_t* out = p.out + fz * fs;
+    // write-through stores of the frame (XCU): one descriptor per wave over
+    // the frame, built from wave-uniform values only
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out, /*stride*/ 0, (int)__builtin_amdgcn_readfirstlane((int)(fs * sizeof(uint16_t))), 0x00020000);
     const uint16_t* prev = TEMP ? (fz ? p.out + (fz - 1) * fs : p.prev) : nullptr;
     const int W = p.W, H = p.H, T = p.T, TT = T + 1;
     const int nbands = (H + 63) / 64, kend = W + 63, stride = W + 64 + 3 * kSync;
     const int prodw = (wv + NW - 1) % NW;
     // (bounded: a broken hand-over shows up as wrong pixels, never as a hang)
+    // XCU: `seen` is the producer's progress as last read; a read is issued
+    // after every wait and consumed at the next one (a round later, so it has
+    // returned), and a wait that `seen` already satisfies costs no load
+    int seen = -1, pending = -1;
     auto wait_ge = [&](int need) {
-        for (int spin = 0; spin < (1 << 24) &&
-                           __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope)) <
-                               need;
-             ++spin)
-            __builtin_amdgcn_s_sleep(1);
-        if constexpr (XCU) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if constexpr (XCU) seen = max(seen, __builtin_amdgcn_readfirstlane(pending));
+        for (int spin = 0; spin < (1 << 24) && seen < need; ++spin) {
+            seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope));
+            if (seen < need) __builtin_amdgcn_s_sleep(1);
+        }
+        if constexpr (XCU) pending = __hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope);
+        // XCU: every later load of the band above's rows is an sc1 load
+        // (hload), so this only keeps the compiler from hoisting them
+        if constexpr (XCU) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    };
-    // the band's stores are complete (in the CU's write-through L1 / the L2)
-    // before its progress is published
-    auto publish = [&](int v) {
-        if constexpr (XCU) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_s_waitcnt(0);
-        if (r == 0) __hip_atomic_store(pos + wv, v, __ATOMIC_RELAXED, kScope);
     };
     auto far = [&](int x, int dx, int dy) -> int {
         const int rr = r + dy;
@@ -459,9 +474,6 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
         const int y = y0 + r;
         const bool row_ok = y < H;
         const int v = y % T, ty = y / T;
-        const uint16_t* srow = sym + (size_t)(row_ok ? y : 0) * W;
-        const uint16_t* prow = TEMP ? prev + (size_t)(row_ok ? y : 0) * W : nullptr;
-        uint16_t* orow = out + (size_t)(row_ok ? y : 0) * W;
         const uint32_t* hsrc = (const uint32_t*)(out + (size_t)(b > 0 && hl ? y0 - TT + hr : 0) * W);
         auto hload = [&](int c0) {  // columns c0 + hc .. + 16 of the round starting at column c0
 #pragma unroll
@@ -477,22 +489,39 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
                     *(uint32_t*)(lds + hand_off + hr * kHand + ((c0 + hc + 2 * q) & (kHand - 1))) = hv[q];
             }
         };
-        // symbols (and previous-frame pixels) in aligned groups of 8 columns:
-        // the current group and the next, loaded 8 columns before its use
-        // (one 16-byte load per lane every 8 steps instead of 8 2-byte loads:
-        // each load instruction touches one line per active lane)
-        // symbols (and previous-frame pixels) in aligned groups of 8 columns:
-        // the current group and the next, loaded 8 columns before its use
-        // (one 16-byte load per lane every 8 steps instead of 8 2-byte loads:
-        // each load instruction touches one line per active lane)
+        // Memory operations are the same for every lane and every round of 8
+        // steps, so the compiler's waits count exactly and none waits for a
+        // fresh operation: lane r handles columns k0 - r .. k0 - r + 7 in the
+        // round starting at step k0, i.e. the aligned 8-column groups g0 and
+        // g0 + 1 (g0 = (k0 - r) >> 3, one more per round).  Symbols (and
+        // previous-frame pixels) sit in a window of four groups G[q & 3] =
+        // group g0 + (slot - q) loaded 3 rounds (24 steps) ahead; the 4 rounds
+        // of a kSync round are unrolled so the window never moves between
+        // registers.  A round starts by storing group g0 - 1 (complete) from
+        // this row's LDS ring with one 16-byte store.  Lanes outside the frame
+        // get an out-of-range buffer offset: the hardware drops the store and
+        // returns zeros for the load.
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         const int ng = W / 8;
-        uint4 scur = *(const uint4*)srow, snxt = *(const uint4*)(srow + 8 * min(1, ng - 1));
-        uint4 pcur{}, pnxt{};
-        if (TEMP) {
-            pcur = *(const uint4*)prow;
-            pnxt = *(const uint4*)(prow + 8 * min(1, ng - 1));
+        const uint32_t sbytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)(fs * sizeof(uint16_t)));
+        const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc((void*)sym, 0, (int)sbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t prsrc =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(TEMP ? prev : sym), 0, (int)sbytes, 0x00020000);
+        constexpr uint32_t kNoOff = 0x7FFFFFF0u;  // past every frame: dropped store / zero load
+        auto goff = [&](int g) -> int {         // byte offset of group g of this lane's row
+            return (row_ok && g >= 0 && g < ng) ? (int)(((uint32_t)y * (uint32_t)W + 8u * (uint32_t)g) * 2u) : (int)kNoOff;
+        };
+        auto gload = [&](const __amdgpu_buffer_rsrc_t& rs, int g) -> u32x4 {
+            return __builtin_amdgcn_raw_buffer_load_b128(rs, goff(g), 0, 0);
+        };
+        const int gbase = (0 - r) >> 3;  // g0 of the first round (floor)
+        u32x4 G[4], Pg[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            G[q] = gload(srsrc, gbase + q);
+            if (TEMP) Pg[q] = gload(prsrc, gbase + q);
         }
-        uint32_t ob0 = 0, ob1 = 0, ob2 = 0, ob3 = 0;  // the output group being filled
+        const int ph = (-r) & 7;  // column offset of step 0 of a round inside group g0
         int u = 0, tx = 0;
         int p1 = 0, p2 = 0;
         auto load_far = [&](NbVals& f, int x) {
@@ -507,75 +536,110 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
             f.v[NB_BAP] = lds[far(x, -T, -1)];
         };
         if (b > 0) {  // the first two rounds' columns of the band above
-            wait_ge((b - 1) * stride + min(2 * kSync + 72, kend));
+            wait_ge((b - 1) * stride + min(kSync + 72, kend));
             hload(0);
             hstore(0);
-            hload(kSync);
-            hstore(kSync);
         }
         NbVals nf;
         nf.v[NB_A] = 0;
         load_far(nf, -r);
         const int edge_k = T + 63;  // before this step some lane has x < T
-        for (int k0 = 0; k0 < kend; k0 += kSymAhead) {
-            if ((k0 & (kSync - 1)) == 0) {
-                publish(b * stride + k0);
-                if (b > 0) {
-                    if (k0 > 0) hstore(k0 + kSync);  // loaded last round
-                    wait_ge((b - 1) * stride + min(k0 + 3 * kSync + 72, kend));
-                    hload(k0 + 2 * kSync);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kSymAhead; ++j) {
-                const int k = k0 + j;
-                const int x = k - r;
-                const int xs = x & 7;
-                auto pick = [&](const uint4& q) {  // column xs of the group (two 64-bit halves
-                    // and a shift: a select chain here became a dynamically indexed stack copy)
-                    const uint64_t a = ((uint64_t)q.y << 32) | q.x, c = ((uint64_t)q.w << 32) | q.z;
-                    return (uint32_t)(((xs & 4) ? c : a) >> (16 * (xs & 3))) & 0xFFFFu;
-                };
-                const uint32_t sv = pick(scur), pv = TEMP ? pick(pcur) : 0u;
-                const bool ok = row_ok && x >= 0 && x < W;
-                NbVals g = nf;
-                load_far(nf, x + 1);
-                g.v[NB_A] = p1;
-                g.v[NB_B] = __builtin_amdgcn_update_dpp(g.v[NB_B], p1, 0x138, 0xF, 0xF, false);
-                g.v[NB_C] = __builtin_amdgcn_update_dpp(g.v[NB_C], p2, 0x138, 0xF, 0xF, false);
-                const int res = unsymbolize16(sv);
-                const int P = TEMP ? (int)pv : 0;
-                int val;
-                if (k >= edge_k && y0 > 0) val = inv_tile3<FAM, K, TC_XY, TEMP>(g, res, P, u, v);
-                else val = inv_edge3<FAM, K, TEMP>(g, res, P, u, v, tx, ty, k >= edge_k);
-                const uint16_t o = (uint16_t)val;
-                if (ok) {
-                    lds[ring_off + r * kRing + (x & (kRing - 1))] = o;
-                    const uint32_t ov = o;
-                    ob0 = xs == 0 ? ov : xs == 1 ? ob0 | ov << 16 : ob0;
-                    ob1 = xs == 2 ? ov : xs == 3 ? ob1 | ov << 16 : ob1;
-                    ob2 = xs == 4 ? ov : xs == 5 ? ob2 | ov << 16 : ob2;
-                    ob3 = xs == 6 ? ov : xs == 7 ? ob3 | ov << 16 : ob3;
-                    if (xs == 7) {  // the group is complete: one 16-byte store, next symbols
-                        *(uint4*)(orow + x - 7) = uint4{ob0, ob1, ob2, ob3};
-                        const int gn = min(x / 8 + 2, ng - 1);
-                        scur = snxt;
-                        snxt = *(const uint4*)(srow + 8 * gn);
-                        if (TEMP) {
-                            pcur = pnxt;
-                            pnxt = *(const uint4*)(prow + 8 * gn);
-                        }
-                    }
-                    if (++u == T) {
-                        u = 0;
-                        ++tx;
-                    }
-                }
-                p2 = p1;
-                p1 = (int)o;
+        unsigned long long* tr = nullptr;
+        if constexpr (XCU) {
+            if (p.trace) {
+                tr = p.trace + (size_t)blockIdx.x * kTraceSlots;
+                if (r == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
             }
         }
-        publish(b * stride + kend);
+        // the last round (k0 = W + 64) only stores every row's last group
+        for (int ks = 0; ks < W + 72; ks += kSync) {
+            {
+                const int rd = ks / kSync;
+                if (tr && r == 0 && 2 + 2 * rd < kTraceSlots) tr[1 + 2 * rd] = __builtin_amdgcn_s_memrealtime();
+                // every store issued before the last round has completed: the
+                // pixels of steps < ks - 24 are in memory (a pixel of step s is
+                // stored by the round starting at <= s + 15)
+                if constexpr (XCU) {
+                    if constexpr (TEMP) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                } else {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_s_waitcnt(0);
+                }
+                if (r == 0) __hip_atomic_store(pos + wv, b * stride + ks - 24, __ATOMIC_RELAXED, kScope);
+                if (b > 0) {  // stored into the LDS ring at the end of this round
+                    wait_ge((b - 1) * stride + min(ks + 2 * kSync + 72, kend));
+                    hload(ks + kSync);
+                }
+                if (tr && r == 0 && 2 + 2 * rd < kTraceSlots) tr[2 + 2 * rd] = __builtin_amdgcn_s_memrealtime();
+            }
+#pragma unroll
+            for (int q = 0; q < kSync / 8; ++q) {
+                const int k0 = ks + 8 * q;
+                const int g0 = (k0 - r) >> 3;
+                asm volatile("" ::: "memory");  // keeps each round's memory operations in their round
+                {   // group g0 - 1 is complete: LDS ring -> one 16-byte store
+                    const int gs = g0 - 1;
+                    const u32x4 ov4 = *(const u32x4*)(lds + ring_off + r * kRing + ((8 * gs) & (kRing - 1)));
+                    __builtin_amdgcn_raw_buffer_store_b128(ov4, orsrc, goff(gs), 0, XCU ? 16 /*sc1*/ : 0);
+                }
+                const u32x4 Ga = G[q & 3], Gb = G[(q + 1) & 3];
+                const u32x4 Pa = TEMP ? Pg[q & 3] : Ga, Pb = TEMP ? Pg[(q + 1) & 3] : Gb;
+                if (k0 < kend) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int k = k0 + j;
+                        const int x = k - r;
+                        const int o = ph + j;  // 0..14: column of the pair (Ga, Gb)
+                        auto pick = [&](const u32x4& qa, const u32x4& qb) {  // two 64-bit halves and a shift
+                            const bool hi = o >= 8;
+                            const uint32_t w0 = hi ? qb.x : qa.x, w1 = hi ? qb.y : qa.y;
+                            const uint32_t w2 = hi ? qb.z : qa.z, w3 = hi ? qb.w : qa.w;
+                            const uint64_t lo64 = ((uint64_t)w1 << 32) | w0, hi64 = ((uint64_t)w3 << 32) | w2;
+                            return (uint32_t)((((o & 4) ? hi64 : lo64) >> (16 * (o & 3)))) & 0xFFFFu;
+                        };
+                        const uint32_t sv = pick(Ga, Gb), pv = TEMP ? pick(Pa, Pb) : 0u;
+                        const bool ok = row_ok && x >= 0 && x < W;
+                        NbVals g = nf;
+                        load_far(nf, x + 1);
+                        g.v[NB_A] = p1;
+                        g.v[NB_B] = __builtin_amdgcn_update_dpp(g.v[NB_B], p1, 0x138, 0xF, 0xF, false);
+                        g.v[NB_C] = __builtin_amdgcn_update_dpp(g.v[NB_C], p2, 0x138, 0xF, 0xF, false);
+                        const int res = unsymbolize16(sv);
+                        const int P = TEMP ? (int)pv : 0;
+                        int val;
+                        if (k >= edge_k && y0 > 0) val = inv_tile3<FAM, K, TC_XY, TEMP>(g, res, P, u, v);
+                        else val = inv_edge3<FAM, K, TEMP>(g, res, P, u, v, tx, ty, k >= edge_k);
+                        const uint16_t o16 = (uint16_t)val;
+                        if (ok) {
+                            lds[ring_off + r * kRing + (x & (kRing - 1))] = o16;
+                            if (++u == T) {
+                                u = 0;
+                                ++tx;
+                            }
+                        }
+                        p2 = p1;
+                        p1 = (int)o16;
+                    }
+                }
+                // group g0 is used up: its slot takes group g0 + 4
+                G[q & 3] = gload(srsrc, g0 + 4);
+                if (TEMP) Pg[q & 3] = gload(prsrc, g0 + 4);
+                // the hand-over columns loaded at the start of this round
+                // (24 steps ago) are first read (lanes r <= T, one step ahead)
+                // at step ks + kSync - 1; their ring slots held columns
+                // < ks - 64, no longer read
+                if (q == kSync / 8 - 2 && b > 0) hstore(ks + kSync);
+            }
+        }
+        // every row's groups are stored: drain, then the band is complete
+        if constexpr (XCU) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_s_waitcnt(0);
+        }
+        if (r == 0) __hip_atomic_store(pos + wv, b * stride + kend, __ATOMIC_RELAXED, kScope);
+        if (tr && r == 0) tr[kTraceSlots - 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -649,7 +713,8 @@ static bool band2_ok(const UnFrames& p)
 // aligned 8-column groups, so W is a multiple of 8)
 static int band4_waves(const UnFrames& p)
 {
-    if (p.T < 2 || p.T > 30 || (p.W & 7) || std::getenv("LFM_UNPREDICT_V3") ||
+    // (band4 / band5 address a frame through 31-bit buffer offsets)
+    if (p.T < 2 || p.T > 30 || (p.W & 7) || (size_t)p.W * p.H * 2 >= 0x7FFFFFF0u || std::getenv("LFM_UNPREDICT_V3") ||
         std::getenv("LFM_UNPREDICT_V2"))
         return 0;
     static const int cap = [] {
@@ -680,12 +745,29 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
         const size_t pbytes = (size_t)grid * nbands * sizeof(int);
         if (hipMallocAsync((void**)&pos, pbytes, st) != hipSuccess) return hipErrorOutOfMemory;
         hipError_t e = hipMemsetAsync(pos, 0xFF, pbytes, st);  // -1: no progress yet
+        static const char* trace_path = std::getenv("LFM_UNPREDICT_TRACE");
+        UnFrames pt = p;
+        const size_t tbytes = (size_t)grid * nbands * kTraceSlots * sizeof(unsigned long long);
+        if (trace_path && e == hipSuccess && hipMalloc((void**)&pt.trace, tbytes) == hipSuccess)
+            e = hipMemsetAsync(pt.trace, 0, tbytes, st);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL((unpredict_band5<FAM, K_>), dim3(grid * nbands), dim3(64), lds, st, p, pos, nbands,
+            hipLaunchKernelGGL((unpredict_band5<FAM, K_>), dim3(grid * nbands), dim3(64), lds, st, pt, pos, nbands,
                                grid);
             e = hipGetLastError();
         }
         (void)hipFreeAsync(pos, st);
+        if (pt.trace) {  // diagnostics: [int32 nfr, int32 nbands, int32 slots][u64 per slot]
+            std::vector<unsigned long long> h(tbytes / sizeof(unsigned long long));
+            if (e == hipSuccess) e = hipMemcpyAsync(h.data(), pt.trace, tbytes, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            (void)hipFree(pt.trace);
+            if (FILE* f = e == hipSuccess ? std::fopen(trace_path, "ab") : nullptr) {
+                const int hd[3] = {grid, nbands, kTraceSlots};
+                std::fwrite(hd, sizeof(hd), 1, f);
+                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                std::fclose(f);
+            }
+        }
         return e;
     }
     if (const int nw = band4_waves(p)) {
@@ -747,7 +829,7 @@ extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, 
     const bool any_temporal = video && (nframes > 1 || (z0 & 1));
     if (any_temporal && family != 0) return LFM_HIP_ENOTINV;  // ((I - pred) + P) >> 1 drops a bit
     if (video && (z0 & 1) && !d_prev) return LFM_HIP_EINVAL;
-    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1};
+    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, nullptr};
     // without video every frame is spatial: one launch; with video the
     // spatial (even global z) frames first, then the temporal ones on their
     // decoded predecessors
