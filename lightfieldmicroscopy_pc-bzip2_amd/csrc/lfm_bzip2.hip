@@ -828,15 +828,34 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     const uint8_t* T = B.T + (size_t)s * B.cap;
     uint64_t k[IPT];
     uint32_t v[IPT];
+    // every load unconditional (clamped indices), all of one kind issued
+    // before any is used: one memory round trip for the values and one for
+    // the text of all IPT items (under per-item branches the compiler waited
+    // for each item's loads in turn: 2 IPT round trips)
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) v[q] = B.vals_a[cb + min(q * TH + t, m ? m - 1u : 0u)];
+    uint32_t d[IPT][3];
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = q * TH + t;
-        v[q] = j < m ? B.vals_a[cb + j] : 0u;
+        const uint32_t i = v[q] & kIdxMask;
+        const uint32_t* w = (const uint32_t*)(T + ((i + 8u <= n ? i : 0u) & ~3u));
+        d[q][0] = w[0];
+        d[q][1] = w[1];
+        d[q][2] = w[2];
     }
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = q * TH + t;
-        k[q] = j < m ? rot_key8_fast(T, n, v[q] & kIdxMask) : ~0ull;
+        const uint32_t j = q * TH + t, i = v[q] & kIdxMask;
+        if (j >= m) {
+            k[q] = ~0ull;
+            v[q] = 0u;
+        } else if (i + 8u <= n) {  // rot_key8_fast's fast path on the loaded dwords
+            const uint32_t sh = (i & 3u) * 8u;
+            const uint64_t x = (uint64_t)d[q][0] | ((uint64_t)d[q][1] << 32);
+            k[q] = __builtin_bswap64(sh ? (x >> sh) | ((uint64_t)d[q][2] << (64u - sh)) : x);
+        } else {
+            k[q] = rot_key8_fast(T, n, i);
+        }
     }
     // the sort's valid-item count refers to the blocked arrangement
     ExK().striped_to_blocked(k, k, sm.ek);
@@ -1976,7 +1995,8 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         s_carry = 0;
         s_wr = 0;
     }
-    uint32_t nrun[2] = {0, 0};  // RUNA / RUNB, the hottest symbols, counted here
+    uint32_t nrunA = 0, nrunB = 0;  // RUNA / RUNB, the hottest symbols, counted here (two scalars:
+                                    // an array indexed by the symbol lived in scratch memory)
     // zero-run scan element: (trailing zeros, all zeros); a then b
     auto zcomb = [](uint32_t atz, uint32_t aaz, uint32_t btz, uint32_t baz, uint32_t& rtz, uint32_t& raz) {
         rtz = baz ? atz + btz : btz;
@@ -2007,10 +2027,14 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
                 if (i < len) f((q[i >> 2] >> (8 * (i & 3))) & 0xFFu);
         };
         // chunk summary: trailing zeros, all-zero (empty chunks pass the carry through)
+        // (the per-value updates are selects: with `++x` in one branch and
+        // `++y` in the other the compiler merged them into one store through
+        // a selected pointer and kept the counters in scratch memory)
         uint32_t tz = 0, az = 1;
         each([&](uint32_t v) {
-            if (v == 0) ++tz;
-            else { tz = 0; az = 0; }
+            const bool zv = v == 0;
+            tz = zv ? tz + 1 : 0u;
+            az = zv ? az : 0u;
         });
         // inclusive scan over the wave, then the waves before
         uint32_t itz = tz, iaz = az;
@@ -2036,9 +2060,10 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         const bool has_last = last_tile && len && c1 == n;
         uint32_t z = carry, w = 0;
         each([&](uint32_t v) {
-            if (v == 0) { ++z; return; }
-            if (z) { w += run_digits(z); z = 0; }
-            ++w;
+            const bool zv = v == 0;
+            const uint32_t d = z ? run_digits(z) : 0u;
+            w = zv ? w : w + d + 1u;
+            z = zv ? z + 1u : 0u;
         });
         if (has_last) {
             if (z) w += run_digits(z);
@@ -2060,8 +2085,12 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         }
         auto emit = [&](uint32_t v) {
             tile_out[wr++] = (uint16_t)v;
-            if (v < 2) ++nrun[v];
-            else atomicAdd(&freq[v], 1u);
+            if (v < 2) {
+                nrunA += v == 0;
+                nrunB += v == 1;
+            } else {
+                atomicAdd(&freq[v], 1u);
+            }
         };
         auto zeros = [&](uint32_t zz) {
             uint32_t zp = zz - 1;
@@ -2073,9 +2102,11 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         };
         z = carry;
         each([&](uint32_t v) {
-            if (v == 0) { ++z; return; }
-            if (z) { zeros(z); z = 0; }
-            emit(v + 1);
+            if (v != 0) {
+                if (z) zeros(z);
+                emit(v + 1);
+            }
+            z = v == 0 ? z + 1u : 0u;
         });
         if (has_last) {
             if (z) zeros(z);
@@ -2094,7 +2125,7 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
     static_assert(kRunA == 0 && kRunB == 1, "RUNA / RUNB are symbols 0 and 1");
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-        uint32_t c = nrun[r];
+        uint32_t c = r ? nrunB : nrunA;
         for (int d = 32; d > 0; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d);
         if (lane == 0 && c) atomicAdd(&freq[r], c);
     }
