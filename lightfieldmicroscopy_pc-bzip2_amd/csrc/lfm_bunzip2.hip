@@ -793,16 +793,45 @@ __device__ __forceinline__ uint32_t crc_xpow8(uint32_t L)
 
 constexpr int kRleSeg = 16;  // segment alignment (bytes)
 
-// per-lane sequential reader of the RLE1 text, 16 bytes at a time with the
-// next chunk loaded one chunk ahead
+// per-lane sequential reader of the RLE1 text, 16 bytes at a time.  The load
+// is unconditional (clamped address, zeros selected past the end): a load
+// under a branch, or a chunk moved between registers while its load is in
+// flight, made the compiler wait for it right away.
 struct TextChunks {
     const uint8_t* p;
     uint32_t cap;
     __device__ __forceinline__ uint4 load(uint32_t at) const
     {
-        return at < cap ? *(const uint4*)(p + at) : uint4{0u, 0u, 0u, 0u};
+        const uint4 v = *(const uint4*)(p + min(at, cap - 16u));
+        return at < cap ? v : uint4{0u, 0u, 0u, 0u};
     }
 };
+
+// visit this lane's 16-byte chunks at a, a + 16, ... while < b, with four
+// chunk registers in rotation, each reloaded three chunks ahead of its use.
+// The loop runs the wave's largest chunk count (a lane past its own end
+// skips f but keeps loading, clamped): no divergent exit and no chunk moved
+// between registers, so the compiler can count its waits.
+template <typename Ld, typename F>
+__device__ __forceinline__ void for_chunks4(uint32_t a, uint32_t b, Ld&& ld, F&& f)
+{
+    const uint32_t nc = b > a ? (b - a + 15u) / 16u : 0u;
+    uint32_t N = nc;
+    for (int d = 32; d > 0; d >>= 1) N = max(N, (uint32_t)__shfl_xor((int)N, d));
+    N = (uint32_t)__builtin_amdgcn_readfirstlane((int)N);
+    uint4 q0 = ld(a), q1 = ld(a + 16), q2 = ld(a + 32), q3 = ld(a + 48);
+    for (uint32_t k = 0; k < N; k += 4) {
+        const uint32_t i = a + 16u * k;
+        if (k < nc) f(q0, i);
+        q0 = ld(i + 64);
+        if (k + 1 < nc) f(q1, i + 16);
+        q1 = ld(i + 80);
+        if (k + 2 < nc) f(q2, i + 32);
+        q2 = ld(i + 96);
+        if (k + 3 < nc) f(q3, i + 48);
+        q3 = ld(i + 112);
+    }
+}
 
 __device__ __forceinline__ uint32_t chunk_byte(const uint4& q, int j)  // j compile-time after unrolling
 {
@@ -829,48 +858,42 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
     const uint32_t seg = ((n + 63) / 64 + kRleSeg - 1) / kRleSeg * kRleSeg;
     const uint32_t a = min(n, lane * seg), b = min(n, a + seg);
     const uint32_t before = a ? (uint32_t)rle[a - 1] : 256u;  // the text byte before the segment
-    // A: all five start states
+    // A: all five start states until their paths meet, then one path
     {
         uint32_t st[5] = {0, 1, 2, 3, 4}, cnt[5] = {0, 0, 0, 0, 0};
-        uint32_t prevb = before;
-        uint32_t i = a;
+        uint32_t prevb = before, s1 = 0, c1 = 0;
         bool met = false;
-        uint4 q = tx.load(a), nq = tx.load(a + 16);
-        for (; i < b && !met; i += 16) {
+        for_chunks4(a, b, [&](uint32_t at) { return tx.load(at); }, [&](const uint4& q, uint32_t i) {
+            if (!met) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (i + j < b) {
-                    const uint32_t c = chunk_byte(q, j);
-                    const bool eq = c == prevb;
+                for (int j = 0; j < 16; ++j) {
+                    if (i + j < b) {
+                        const uint32_t c = chunk_byte(q, j);
+                        const bool eq = c == prevb;
 #pragma unroll
-                    for (int p = 0; p < 5; ++p) {
-                        const bool c4 = st[p] == 4;
-                        cnt[p] += c4 ? c : 1u;
-                        st[p] = c4 ? 0u : ((st[p] == 0 || !eq) ? 1u : st[p] + 1u);
+                        for (int p = 0; p < 5; ++p) {
+                            const bool c4 = st[p] == 4;
+                            cnt[p] += c4 ? c : 1u;
+                            st[p] = c4 ? 0u : ((st[p] == 0 || !eq) ? 1u : st[p] + 1u);
+                        }
+                        prevb = c;
                     }
-                    prevb = c;
                 }
-            }
-            q = nq;
-            nq = tx.load(i + 32);
-            met = st[0] == st[1] && st[0] == st[2] && st[0] == st[3] && st[0] == st[4];
-        }
-        // the paths have met (or the segment is done): one path for the rest
-        uint32_t s1 = st[0], c1 = 0;
-        for (; i < b; i += 16) {
+                met = st[0] == st[1] && st[0] == st[2] && st[0] == st[3] && st[0] == st[4];
+                s1 = st[0];
+            } else {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (i + j < b) {
-                    const uint32_t c = chunk_byte(q, j);
-                    const bool c4 = s1 == 4;
-                    c1 += c4 ? c : 1u;
-                    s1 = c4 ? 0u : ((s1 == 0 || c != prevb) ? 1u : s1 + 1u);
-                    prevb = c;
+                for (int j = 0; j < 16; ++j) {
+                    if (i + j < b) {
+                        const uint32_t c = chunk_byte(q, j);
+                        const bool c4 = s1 == 4;
+                        c1 += c4 ? c : 1u;
+                        s1 = c4 ? 0u : ((s1 == 0 || c != prevb) ? 1u : s1 + 1u);
+                        prevb = c;
+                    }
                 }
             }
-            q = nq;
-            nq = tx.load(i + 32);
-        }
+        });
         uint32_t map = 0;
 #pragma unroll
         for (int p = 0; p < 5; ++p) {
@@ -929,8 +952,7 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
             }
             ++o;
         };
-        uint4 q = tx.load(a), nq = tx.load(a + 16);
-        for (uint32_t i = a; i < b; i += 16) {
+        for_chunks4(a, b, [&](uint32_t at) { return tx.load(at); }, [&](const uint4& q, uint32_t i) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 if (i + j < b) {
@@ -945,9 +967,7 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
                     prevb = c;
                 }
             }
-            q = nq;
-            nq = tx.load(i + 32);
-        }
+        });
     }
     // the other lanes' bytes are read back below (same wave, L1 write-through)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -959,14 +979,17 @@ __global__ __launch_bounds__(64) void bzd_rle1(Dec D)
     const int64_t e = (int64_t)tot - (int64_t)(63 - lane) * segc;
     const uint32_t c0 = (uint32_t)max<int64_t>(0, e - (int64_t)segc), c1 = (uint32_t)max<int64_t>(0, e);
     uint32_t r = 0;
-    {  // aligned words (the word holding a valid byte lies in its page)
-        uint32_t w = 0;
-        for (uint32_t i = c0; i < c1; ++i) {
-            const uintptr_t ua = (uintptr_t)(out + i);
-            if (i == c0 || (ua & 3) == 0) w = *(const uint32_t*)(ua & ~(uintptr_t)3);
-            const uint32_t c = (w >> (8 * (ua & 3))) & 0xFFu;
-            r = (r << 8) ^ T1[(r >> 24) ^ c];
-        }
+    if (c1 > c0) {  // aligned 16-byte chunks (a chunk holding a valid byte lies in its page)
+        const uintptr_t u0 = (uintptr_t)(out + c0), u1 = (uintptr_t)(out + c1);
+        const uintptr_t first = u0 & ~(uintptr_t)15, last = (u1 - 1) & ~(uintptr_t)15;
+        const uint32_t nb = (uint32_t)(last - first) + 16u;  // bytes of the chunks
+        auto ld = [&](uint32_t at) { return *(const uint4*)(first + min((uintptr_t)at, last - first)); };
+        const uint32_t lo = (uint32_t)(u0 - first), hi = (uint32_t)(u1 - first);
+        for_chunks4(0u, nb, ld, [&](const uint4& q, uint32_t i) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (i + j >= lo && i + j < hi) r = (r << 8) ^ T1[(r >> 24) ^ chunk_byte(q, j)];
+        });
     }
     uint32_t X = crc_xpow8(segc);  // wave-uniform
     for (int j = 0; j < 6; ++j) {

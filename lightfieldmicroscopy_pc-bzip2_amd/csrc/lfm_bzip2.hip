@@ -254,7 +254,9 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
 {
     constexpr uint32_t NW = kRleThreads / 64;
     __shared__ uint32_t crc4[4][256];
-    __shared__ uint8_t tout[kRleTile + kRleTile / 4 + 64];
+    // the tile's RLE1 bytes at tout[po ..), po = the stream offset mod 16:
+    // tout[0 .. po) holds the previous tile's last partial 16-byte unit
+    __shared__ __attribute__((aligned(16))) uint8_t tout[16 + kRleTile + kRleTile / 4 + 64];
     __shared__ RunSum wrs[NW];
     __shared__ uint32_t wcnt[NW], wcrc[NW];
     __shared__ RunSum s_carry;
@@ -405,12 +407,12 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
         if (lane == 0) wcrc[wave] = cc;
         __syncthreads();
-        uint32_t base = cinc - cnt, total = 0;
+        const uint32_t wr0 = s_wr, po = wr0 & 15u;
+        uint32_t base = po + cinc - cnt, total = 0;
         for (uint32_t w2 = 0; w2 < NW; ++w2) {
             if (w2 < wave) base += wcnt[w2];
             total += wcnt[w2];
         }
-        const uint32_t wr0 = s_wr;
         walk([&](uint32_t c, uint32_t l) {
             const uint8_t b = (uint8_t)c;
             if (l >= 4) {
@@ -435,8 +437,16 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             ncrc = gf2_apply(c_crc_shift[9], s_crc) ^ tc;
         }
         __syncthreads();
-        for (uint32_t i = t; i < total; i += kRleThreads)
-            if (wr0 + i < wlim) Tout[wr0 + i] = tout[i];
+        // whole 16-byte units out (16-byte stores; a unit starting before
+        // wlim ends inside the 256-aligned cap), the last partial unit kept
+        {
+            const uint32_t end = po + total, full = end >> 4, ub = wr0 & ~15u;
+            for (uint32_t u = t; u < full; u += kRleThreads)
+                if (ub + 16u * u < wlim) *(uint4*)(Tout + ub + 16u * u) = *(const uint4*)(tout + 16u * u);
+            const uint8_t keep = t < 16u ? tout[16u * full + t] : (uint8_t)0;
+            __syncthreads();
+            if (t < 16u) tout[t] = keep;
+        }
         if (t == 0) {
             s_carry = ncarry;
             s_crc = ncrc;
@@ -444,6 +454,10 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
     }
     __syncthreads();
+    {  // the stream's last partial unit (bytes past the end are not read)
+        const uint32_t wr = s_wr;
+        if ((wr & 15u) && t == 0 && (wr & ~15u) < wlim) *(uint4*)(Tout + (wr & ~15u)) = *(const uint4*)tout;
+    }
     if (t == 0) {
         const uint32_t total = s_wr;
         uint32_t crc = s_crc;
