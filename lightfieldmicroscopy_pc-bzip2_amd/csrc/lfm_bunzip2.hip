@@ -588,23 +588,49 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
 // ------------------------------------------------------------ inverse BWT --
 constexpr int kTtThreads = 256;
 
+// ll is read 16 bytes per thread, a step ahead, with every load
+// unconditional (clamped) and loop trip counts uniform: the byte-per-thread
+// loads of a tile, each used right away, made all three passes wait one
+// memory latency per 256 positions (ll and tt live in 256-aligned stream
+// regions of cap bytes / words, so whole 16-byte chunks up to n stay inside)
 template <int NT>
 __global__ __launch_bounds__(NT) void bzd_tt(Dec D)
 {
+    constexpr uint32_t kBlk = 16u * NT;  // ll bytes per staged block (16 tiles)
     __shared__ uint32_t cf[256];       // C[c]: bytes < c
     __shared__ uint32_t run[256];      // occurrences of c before the current tile
     __shared__ uint32_t wc[NT / 64][256];
+    __shared__ __attribute__((aligned(16))) uint8_t sll[kBlk];
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (D.flags[s]) return;
     const uint32_t n = D.n[s];
     const uint8_t* ll = D.ll + (size_t)s * D.cap;
     uint32_t* tt = D.tt + (size_t)s * D.cap;
+    const uint32_t nch = (n + 15u) / 16u;  // 16-byte chunks of ll
+    auto ldc = [&](uint32_t ci) { return *(const uint4*)(ll + 16u * min(ci, nch ? nch - 1u : 0u)); };
     for (uint32_t c = t; c < 256; c += NT) {
         run[c] = 0;
         for (int w = 0; w < NT / 64; ++w) wc[w][c] = 0;
     }
     __syncthreads();
-    for (uint32_t i = t; i < n; i += NT) atomicAdd(&run[ll[i]], 1u);
+    {  // byte counts: chunk k * NT + t in step k, two chunk registers in turn
+        const uint32_t K = (nch + NT - 1u) / NT;
+        auto count = [&](const uint4& q, uint32_t ci) {
+            if (ci < nch) {
+                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (16u * ci + j < n) atomicAdd(&run[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+            }
+        };
+        uint4 qa = ldc(t), qb = ldc(NT + t);
+        for (uint32_t k = 0; k < K; k += 2) {
+            count(qa, k * NT + t);
+            qa = ldc((k + 2) * NT + t);
+            count(qb, (k + 1) * NT + t);
+            qb = ldc((k + 3) * NT + t);
+        }
+    }
     __syncthreads();
     if (t < 64) {  // exclusive scan of the 256 counts, 4 per lane
         uint32_t v[4], sum = 0;
@@ -625,42 +651,70 @@ __global__ __launch_bounds__(NT) void bzd_tt(Dec D)
     }
     __syncthreads();
     for (uint32_t c = t; c < 256; c += NT) run[c] = 0;
-    __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
-    // LF(i) = C[c] + Occ(c, i) in tiles of NT positions
-    for (uint32_t i0 = 0; i0 < n; i0 += NT) {
-        const uint32_t i = i0 + t;
-        const bool ok = i < n;
-        const uint32_t c = ok ? ll[i] : 256u;
-        uint64_t mm = __ballot(ok);
+    // LF(i) = C[c] + Occ(c, i) in tiles of NT positions; ll staged in LDS a
+    // block of 16 tiles at a time, the next block's chunk loaded meanwhile
+    uint4 nb = ldc(t);
+    for (uint32_t b0 = 0; b0 < n; b0 += kBlk) {
+        __syncthreads();  // the previous block's tiles have read sll
+        *(uint4*)(sll + 16u * t) = nb;
+        nb = ldc((b0 + kBlk) / 16u + t);
+        __syncthreads();
+        for (uint32_t i0 = b0; i0 < min(n, b0 + kBlk); i0 += NT) {
+            const uint32_t i = i0 + t;
+            const bool ok = i < n;
+            const uint32_t c = ok ? (uint32_t)sll[i - b0] : 256u;
+            uint64_t mm = __ballot(ok);
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const uint64_t bb = __ballot(ok && ((c >> b) & 1u));
-            mm &= ((c >> b) & 1u) ? bb : ~bb;
-        }
-        const uint32_t rw = (uint32_t)__popcll(mm & lt);
-        const bool leader = ok && (mm & lt) == 0;
-        if (leader) wc[wave][c] = (uint32_t)__popcll(mm);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        if (ok) {
-            for (uint32_t w = 0; w < NT / 64; ++w) {
-                const uint32_t x = wc[w][c];
-                before += w < wave ? x : 0u;
-                total += x;
+            for (int b = 0; b < 8; ++b) {
+                const uint64_t bb = __ballot(ok && ((c >> b) & 1u));
+                mm &= ((c >> b) & 1u) ? bb : ~bb;
             }
-            const uint32_t lf = cf[c] + run[c] + before + rw;
-            tt[lf] = i;
+            const uint32_t rw = (uint32_t)__popcll(mm & lt);
+            const bool leader = ok && (mm & lt) == 0;
+            if (leader) wc[wave][c] = (uint32_t)__popcll(mm);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+            if (ok) {
+                for (uint32_t w = 0; w < NT / 64; ++w) {
+                    const uint32_t x = wc[w][c];
+                    before += w < wave ? x : 0u;
+                    total += x;
+                }
+                const uint32_t lf = cf[c] + run[c] + before + rw;
+                tt[lf] = i;
+            }
+            __syncthreads();
+            // the last occurrence of c in the tile advances the running count
+            if (ok && before + rw + 1 == total) run[c] += total;
+            if (leader) wc[wave][c] = 0;
+            __syncthreads();
         }
-        __syncthreads();
-        // the last occurrence of c in the tile advances the running count
-        if (ok && before + rw + 1 == total) run[c] += total;
-        if (leader) wc[wave][c] = 0;
-        __syncthreads();
     }
     __syncthreads();
-    // decompress.c's fast tt: tt[j] = next << 8 | ll[j]
-    for (uint32_t j = t; j < n; j += NT) tt[j] = (tt[j] << 8) | ll[j];
+    {  // decompress.c's fast tt: tt[j] = next << 8 | ll[j], 4 entries per thread
+        const uint32_t ng = (n + 3u) / 4u, K = (ng + NT - 1u) / NT;
+        auto ldg = [&](uint32_t g, uint4& v, uint32_t& b) {
+            const uint32_t gc = min(g, ng ? ng - 1u : 0u);
+            v = *(const uint4*)(tt + 4u * gc);
+            b = *(const uint32_t*)(ll + 4u * gc);
+        };
+        auto put = [&](uint32_t g, const uint4& v, uint32_t b) {
+            if (g < ng)
+                *(uint4*)(tt + 4u * g) = make_uint4((v.x << 8) | (b & 0xFFu), (v.y << 8) | ((b >> 8) & 0xFFu),
+                                                    (v.z << 8) | ((b >> 16) & 0xFFu), (v.w << 8) | (b >> 24));
+        };
+        uint4 va, vb;
+        uint32_t ba, bb;
+        ldg(t, va, ba);
+        ldg(NT + t, vb, bb);
+        for (uint32_t k = 0; k < K; k += 2) {
+            put(k * NT + t, va, ba);
+            ldg((k + 2) * NT + t, va, ba);
+            put((k + 1) * NT + t, vb, bb);
+            ldg((k + 3) * NT + t, vb, bb);
+        }
+    }
 }
 
 // marker id of node j (or ~0u): every kMark-th node, and the walk's start
