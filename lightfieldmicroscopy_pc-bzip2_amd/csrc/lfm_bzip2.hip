@@ -267,13 +267,31 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t rowb = sz[0] * B.g.bpp;
     const uint32_t L = rowb * sz[1] * sz[2] * sz[3] * sz[4];
     const uint8_t* raw = B.raw + (size_t)s * B.raw_cap;
+    // divisions by the block's row bytes and extents: float reciprocal and
+    // one correction step (exact for x < 2^23, integer division above): a
+    // 32-bit integer division is ~40 instructions, four per load
+    struct FDiv {
+        uint32_t d;
+        float inv;
+        __device__ __forceinline__ uint32_t div(uint32_t x) const
+        {
+            if (x >= (1u << 23)) return x / d;  // (huge blocks only)
+            uint32_t q = (uint32_t)((float)x * inv);
+            const int32_t r = (int32_t)(x - q * d);
+            q += r >= (int32_t)d ? 1u : 0u;
+            q -= r < 0 ? 1u : 0u;
+            return q;
+        }
+    };
+    const FDiv frow{rowb, 1.0f / (float)rowb}, fy{sz[1], 1.0f / (float)sz[1]}, fz{sz[2], 1.0f / (float)sz[2]},
+        fc{sz[3], 1.0f / (float)sz[3]};
     auto load16 = [&](uint32_t g) -> uint4 {
         if (FROM_IMG) {  // rows are whole 16-byte pieces at 16-byte aligned addresses
-            const uint32_t row = g / rowb, col = g - row * rowb;
-            uint32_t q = row;
-            const uint32_t y = q % sz[1]; q /= sz[1];
-            const uint32_t z = q % sz[2]; q /= sz[2];
-            const uint32_t c = q % sz[3]; q /= sz[3];
+            const uint32_t row = frow.div(g), col = g - row * rowb;
+            uint32_t q = row, qn;
+            qn = fy.div(q); const uint32_t y = q - qn * sz[1]; q = qn;
+            qn = fz.div(q); const uint32_t z = q - qn * sz[2]; q = qn;
+            qn = fc.div(q); const uint32_t c = q - qn * sz[3]; q = qn;
             const size_t src = ((((size_t)(org[4] + q) * B.g.dims[3] + (org[3] + c)) * B.g.dims[2] + (org[2] + z)) *
                                     B.g.dims[1] + (org[1] + y)) * B.g.dims[0] + org[0];
             return *(const uint4*)(B.img + src * B.g.bpp + col);
