@@ -413,6 +413,53 @@ def inproc_leg(local, threads, ndevs):
     return out
 
 
+def torchrun_cmd(n, argv, port):
+    """The child command `bench.py --gpus N` runs when it is not already one
+    rank of an N-rank job: torchrun with N ranks on this node (127.0.0.1
+    rendezvous), bench.py with the same arguments."""
+    return [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+            "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """Start the N rank processes as children (torchrun) and exit with their
+    status.  Called before anything touches the GPU: this process only counts
+    devices (no HIP context) and never execs; rank 0's JSON line reaches the
+    caller through the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.stdout.flush()
+    return subprocess.run(torchrun_cmd(n, argv, port), env=env).returncode
+
+
+def rank_layout(gpus, env, ndev):
+    """(world, rank, local, local_world) of this process, or an error string.
+    --gpus N is authoritative: a process with no WORLD_SIZE and N > 1 launches
+    N ranks (returned as world None), and a rank whose WORLD_SIZE differs from
+    N refuses to run (its line would be labelled with the wrong GPU count)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if gpus > 1:
+            backend = env.get("LFM_BENCH_BACKEND", "nccl")
+            if backend == "nccl" and gpus > ndev:
+                return "--gpus %d but only %d device(s) visible" % (gpus, ndev)
+            return None, 0, 0, gpus
+        if gpus < 1:
+            return "--gpus must be >= 1"
+        return 1, 0, 0, 1
+    world = int(ws)
+    if world != gpus:
+        return "WORLD_SIZE=%d but --gpus %d: the line would misreport the GPU count" % (world, gpus)
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", "0"))
+    return world, rank, local, int(env.get("LOCAL_WORLD_SIZE", str(world)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -427,21 +474,31 @@ def main():
     ap.add_argument("--no-inproc", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # device_count() creates no HIP context on this image: safe before the spawn
+    lay = rank_layout(args.gpus, os.environ, torch.cuda.device_count())
+    if isinstance(lay, str):
+        print("bench.py: " + lay, file=sys.stderr)
+        sys.exit(2)
+    world, rank, local, local_world = lay
+    if world is None:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # LFM_BENCH_BACKEND=gloo rehearses the N-rank path with several ranks on
     # one GPU (local rank modulo the visible devices); the driver's N-GPU runs
     # use nccl (RCCL): the barriers, the slab-size all_gather and the MAX
     backend = os.environ.get("LFM_BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev
     torch.cuda.set_device(local)
+    cpu_group = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # host-side waits while rank 0 drives every device (the inproc leg):
+            # an RCCL barrier would park a spinning kernel on each waiting GPU
+            cpu_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group(backend)
+            cpu_group = dist.group.WORLD
     lfm.require_gpu()
     lfm.set_family(FAMILY)
     zf = args.frames
@@ -578,6 +635,22 @@ def main():
     if world > 1:
         dist.barrier()
         shm.close()
+        if not args.no_inproc:
+            # the drop-in writer over all N devices, driven from rank 0 alone
+            # (what a writeKLBstack / MEX caller on this node gets): every rank
+            # first releases its encoder and device memory
+            enc.close()
+            del d_img
+            sel_frame = None
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            dist.barrier(group=cpu_group)
+            if rank == 0:
+                devs = [r % ndev for r in range(world)]
+                node_threads = min(len(os.sched_getaffinity(0)), threads * local_world)
+                line["inproc"] = inproc_leg(local, node_threads if backend == "nccl" else threads,
+                                            [[local], devs])
+            dist.barrier(group=cpu_group)
     buf = bytes(b) if rank == 0 and world == 1 and not args.no_decode else None  # before b's buffer is reused
     if rank == 0 and world == 1 and not args.no_host_input:
         line["host_input"] = host_input_rates(enc, d_img, zf)

@@ -70,7 +70,9 @@ LFM_API int lfm_encoder_encode(lfm_encoder* enc, const void* img, int img_is_dev
                                lfm_encode_stats* stats);
 
 /* Pipelined encode of a stack (z0 = 0, prev_frame = NULL) or of a z-slab
- * (arguments as lfm_encoder_encode_slab).  Runs the predictor stage (img may
+ * (arguments as lfm_encoder_encode_slab).  An auto request (headerVersion &
+ * 0x7F < 8) on a slab with z0 > 0 returns 3: use lfm_encoder_submit_select
+ * with the stack's frame 0, or a forced request 8 + k.  Runs the predictor stage (img may
  * be released on return), then hands the GPU bzip2 stage, the .lfm assembly
  * and its payload copies (system DMA engine) to a finisher thread and
  * returns.  The next submit's GPU work starts once this encode's kernels are
@@ -108,7 +110,9 @@ LFM_API int lfm_encoder_wait(lfm_encoder* enc, uint64_t ticket, const uint8_t** 
  * k selected on the whole stack's frame 0) so every slab codes like the
  * whole stack would; slab depths must be multiples of the block depth except
  * the last.  The result is a valid .lfm of the slab (lfm_merge_slabs joins
- * them). */
+ * them).  An auto request (headerVersion & 0x7F < 8) with z0 > 0 returns 3:
+ * the slab's own frame 0 is not the stack's, so it cannot select what the
+ * whole-stack encode selects. */
 LFM_API int lfm_encoder_encode_slab(lfm_encoder* enc, const void* img, int img_is_device, const void* prev_frame,
                                     uint32_t z0, const uint32_t xyzct[KLB_DATA_DIMS], int dataType,
                                     int headerVersion, int Nnum, const uint32_t blockSize[KLB_DATA_DIMS],
@@ -137,11 +141,18 @@ LFM_API int lfm_place_slab(const uint8_t* slab, uint64_t slab_len, uint8_t* dst,
 /* Devices the writers farm block ranges to (klb_imageIO::writeImage,
  * writeKLBstack, writeLFMstack_c, lfm_encoder_encode_multi): n > 0 sets the
  * list (a device may repeat: several workers on one GPU); n = 0 restores the
- * default (env LFM_GPUS = "0,1,.." or a count, else the current device in a one-process-per-GPU job (WORLD_SIZE /
- * LOCAL_WORLD_SIZE > 1), else every visible device).
- * lfm_get_devices returns the count and fills up to cap entries. */
+ * default: env LFM_GPUS = "0,1,.." or a count; else, in a multi-process job,
+ * one device when several processes share this node (LOCAL_WORLD_SIZE or
+ * OMPI_COMM_WORLD_LOCAL_SIZE > 1, or only WORLD_SIZE > 1 known): LOCAL_RANK
+ * (OMPI_COMM_WORLD_LOCAL_RANK) modulo the visible devices, the current device
+ * when no local rank is set; else (one process on the node) every visible
+ * device.  lfm_get_devices returns the count and fills up to cap entries. */
 LFM_API int lfm_set_devices(const int* devices, int n);
 LFM_API int lfm_get_devices(int* devices, int cap);
+/* The default list above for n_visible devices and current device `current`
+ * (no device call; what lfm_get_devices gives after lfm_set_devices(NULL, 0)
+ * on such a machine).  Returns the count and fills up to cap entries. */
+LFM_API int lfm_default_devices(int n_visible, int current, int* devices, int cap);
 
 /* Encode a HOST stack on the device list above (one host thread per device,
  * block-layer ranges: z-slabs, or ranges of c / t), into the encoder's

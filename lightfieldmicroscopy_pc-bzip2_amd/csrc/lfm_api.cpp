@@ -158,6 +158,13 @@ extern "C" int lfm_get_devices(int* devices, int cap)
     return (int)d.size();
 }
 
+extern "C" int lfm_default_devices(int n_visible, int current, int* devices, int cap)
+{
+    const std::vector<int> d = lfm::default_devices(n_visible, current);
+    for (int i = 0; i < cap && i < (int)d.size(); ++i) devices[i] = d[i];
+    return (int)d.size();
+}
+
 extern "C" int lfm_encoder_encode_multi(lfm_encoder* e, const void* img, const uint32_t xyzct[KLB_DATA_DIMS],
                                         int dataType, int headerVersion, int Nnum,
                                         const uint32_t blockSize[KLB_DATA_DIMS], int compressionType,

@@ -1405,9 +1405,15 @@ __global__ __launch_bounds__(1024) void bwt_rank0(Batch B)
         const uint32_t j = j0 + t;
         bool head = false, next_head = true;
         if (j < n) {
-            // a slot joins its predecessor's group only while the chunk sort
-            // left it flagged: runs it resolved (tie_run_sort) are final.
-            // Both flags are read before the barrier ahead of the rewrite.
+            // Flag contract: the chunk sort flags every slot whose 8-byte key
+            // equals a neighbour's; tie_runs_direct re-orders such runs from
+            // the text but leaves their flags set, so the rounds below re-sort
+            // them to the same order.  A slot joins its predecessor's group
+            // when it is flagged and its key equals the predecessor's.  Equal
+            // keys never straddle a chunk (chunks end at bucket ends), so an
+            // equal key implies the flag; the flag test only saves the key
+            // comparison for unflagged slots.  Both flags are read before the
+            // barrier ahead of the rewrite.
             const bool fj = B.uflag[o + j] != 0;
             const bool fn = j + 1 < n && B.uflag[o + j + 1] != 0;
             const uint64_t k = K(j);

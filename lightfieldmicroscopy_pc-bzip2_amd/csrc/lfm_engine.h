@@ -217,6 +217,8 @@ void release_pooled_encoders();
 // rank of a one-process-per-GPU job (WORLD_SIZE / LOCAL_WORLD_SIZE > 1), else
 // every visible device
 std::vector<int> encode_devices();
+// the default device list for n visible devices, `current` the caller's device (-1: unknown)
+std::vector<int> default_devices(int n, int current);
 void set_encode_devices(const std::vector<int>& devs);
 
 // Multi-GPU writer (lfm_multigpu.cpp): host image, block-layer ranges farmed

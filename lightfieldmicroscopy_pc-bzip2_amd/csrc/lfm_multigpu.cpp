@@ -55,14 +55,18 @@ void set_encode_devices(const std::vector<int>& devs)
     g_devices = devs;
 }
 
-std::vector<int> encode_devices()
+namespace {
+int env_int(const char* name, int dflt)
 {
-    {
-        std::lock_guard<std::mutex> lk(g_dev_mu);
-        if (!g_devices.empty()) return g_devices;
-    }
-    const int n = lfm_hip_device_count();
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atoi(e) : dflt;
+}
+} // namespace
+
+std::vector<int> default_devices(int n, int current)
+{
     std::vector<int> out;
+    if (n <= 0) return out;
     // LFM_GPUS: "0,1,2,3" (a device list; repeats map several workers onto
     // one device) or "N" (devices 0 .. N-1)
     if (const char* e = std::getenv("LFM_GPUS")) {
@@ -84,19 +88,37 @@ std::vector<int> encode_devices()
         }
         if (!out.empty()) return out;
     }
-    // a process of a one-process-per-GPU job (torchrun / MPI launchers set
-    // these) owns its current device only: farming to every GPU of the node
-    // from each rank would oversubscribe them all
-    for (const char* v : {"LOCAL_WORLD_SIZE", "WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE"}) {
-        const char* e = std::getenv(v);
-        if (e && std::atoi(e) > 1) {
-            int dev = 0;
-            if (n <= 0 || hipGetDevice(&dev) != hipSuccess) dev = 0;
-            return {dev};
-        }
+    // A process of a multi-process job (torchrun / MPI launchers set these).
+    // The number of processes on THIS node decides: one process per node owns
+    // every GPU of it; several share the node, and farming to every GPU from
+    // each of them would oversubscribe them all, so each takes one device --
+    // its local rank modulo the visible devices (the current device is not
+    // trusted: a rank that never called set_device would sit on device 0).
+    // Only a global WORLD_SIZE > 1 with no local size known is taken as
+    // one process per GPU.
+    int local_size = env_int("LOCAL_WORLD_SIZE", -1);
+    if (local_size < 0) local_size = env_int("OMPI_COMM_WORLD_LOCAL_SIZE", -1);
+    const bool shared_node = local_size > 1 || (local_size < 0 && env_int("WORLD_SIZE", 1) > 1);
+    if (shared_node) {
+        int lr = env_int("LOCAL_RANK", -1);
+        if (lr < 0) lr = env_int("OMPI_COMM_WORLD_LOCAL_RANK", -1);
+        if (lr >= 0) return {lr % n};
+        return {(current >= 0 && current < n) ? current : 0};
     }
     for (int i = 0; i < n; ++i) out.push_back(i);
     return out;
+}
+
+std::vector<int> encode_devices()
+{
+    {
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        if (!g_devices.empty()) return g_devices;
+    }
+    const int n = lfm_hip_device_count();
+    int cur = -1;
+    if (n <= 0 || hipGetDevice(&cur) != hipSuccess) cur = -1;
+    return default_devices(n, cur);
 }
 
 // persistent encoders (device buffers kept between calls) keyed by (device,

@@ -74,8 +74,15 @@ struct UnFrames {
     // diagnostics (LFM_UNPREDICT_TRACE): per band5 workgroup, kTraceSlots
     // 100 MHz timestamps (band start, then before / after each round's wait)
     unsigned long long* trace;
+    // band4 / band5 hand-over: a wait gives up after spin_limit polls (a
+    // band that never sees its producer must not hang the device) and then
+    // sets *err (band5: global memory, checked by the launcher, which re-runs
+    // the frames through band4); null = not reported
+    int spin_limit;
+    int* err;
 };
 constexpr int kTraceSlots = 512;
+constexpr int kSpinLimit = 1 << 24;  // ~0.45 s of s_sleep 1 polls
 
 template <int FAM, int K>
 __global__ __launch_bounds__(64) void unpredict_band(UnFrames p)
@@ -441,17 +448,20 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
     const int W = p.W, H = p.H, T = p.T, TT = T + 1;
     const int nbands = (H + 63) / 64, kend = W + 63, stride = W + 64 + 3 * kSync;
     const int prodw = (wv + NW - 1) % NW;
-    // (bounded: a broken hand-over shows up as wrong pixels, never as a hang)
+    // (bounded: a hand-over that times out sets *p.err -- the launcher then
+    // discards the band5 result and re-runs the frames -- never a hang)
     // XCU: `seen` is the producer's progress as last read; a read is issued
     // after every wait and consumed at the next one (a round later, so it has
     // returned), and a wait that `seen` already satisfies costs no load
     int seen = -1, pending = -1;
+    const int spin_limit = p.spin_limit;
     auto wait_ge = [&](int need) {
         if constexpr (XCU) seen = max(seen, __builtin_amdgcn_readfirstlane(pending));
-        for (int spin = 0; spin < (1 << 24) && seen < need; ++spin) {
+        for (int spin = 0; spin < spin_limit && seen < need; ++spin) {
             seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope));
             if (seen < need) __builtin_amdgcn_s_sleep(1);
         }
+        if (seen < need && p.err && r == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (XCU) pending = __hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope);
         // XCU: every later load of the band above's rows is an sc1 load
         // (hload), so this only keeps the compiler from hoisting them
@@ -735,18 +745,31 @@ static bool band5_enabled()
     return on;
 }
 
-template <int FAM, int K_>
-static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
+// hand-over poll limit: kSpinLimit, or LFM_UNPREDICT_SPIN (tests force a
+// timeout with a tiny limit); LFM_UNPREDICT_FALLBACK=0 reports a band5 timeout
+// as an error instead of re-running the frames through band4
+static int spin_limit()
 {
-    if (band4_waves(p) && band5_enabled()) {
+    const char* e = std::getenv("LFM_UNPREDICT_SPIN");
+    return e ? std::max(1, std::atoi(e)) : kSpinLimit;
+}
+
+template <int FAM, int K_>
+static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool no_band5 = false)
+{
+    if (band4_waves(p) && band5_enabled() && !no_band5) {
         const int nbands = (p.H + 63) / 64;
         const size_t lds = (size_t)(64 * kRing + (p.T + 1) * kHand) * 2;
         int* pos = nullptr;
         const size_t pbytes = (size_t)grid * nbands * sizeof(int);
-        if (hipMallocAsync((void**)&pos, pbytes, st) != hipSuccess) return hipErrorOutOfMemory;
+        // progress words, then the timeout word
+        if (hipMallocAsync((void**)&pos, pbytes + sizeof(int), st) != hipSuccess) return hipErrorOutOfMemory;
         hipError_t e = hipMemsetAsync(pos, 0xFF, pbytes, st);  // -1: no progress yet
+        if (e == hipSuccess) e = hipMemsetAsync(pos + (size_t)grid * nbands, 0, sizeof(int), st);
         static const char* trace_path = std::getenv("LFM_UNPREDICT_TRACE");
         UnFrames pt = p;
+        pt.spin_limit = spin_limit();
+        pt.err = pos + (size_t)grid * nbands;
         const size_t tbytes = (size_t)grid * nbands * kTraceSlots * sizeof(unsigned long long);
         if (trace_path && e == hipSuccess && hipMalloc((void**)&pt.trace, tbytes) == hipSuccess)
             e = hipMemsetAsync(pt.trace, 0, tbytes, st);
@@ -755,7 +778,24 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st)
                                grid);
             e = hipGetLastError();
         }
+        // a band that gave up waiting (its producer never got a CU, e.g. the
+        // chip shared with other work) decoded from rows that were not ready:
+        // the launch's result is discarded and every frame re-run through
+        // band4, whose bands share one workgroup and so are co-resident
+        int timed_out = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&timed_out, pt.err, sizeof(int), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
         (void)hipFreeAsync(pos, st);
+        if (e == hipSuccess && timed_out) {
+            static const bool fallback = [] {
+                const char* f = std::getenv("LFM_UNPREDICT_FALLBACK");
+                return !(f && std::atoi(f) == 0);
+            }();
+            std::fprintf(stderr, "lfm: inverse predictor band hand-over timed out (band5, %d x %d bands)%s\n", grid,
+                         nbands, fallback ? "; frames re-run through band4" : "");
+            if (!fallback) e = hipErrorLaunchTimeOut;
+            else e = launch_band2<FAM, K_>(p, grid, st, true);
+        }
         if (pt.trace) {  // diagnostics: [int32 nfr, int32 nbands, int32 slots][u64 per slot]
             std::vector<unsigned long long> h(tbytes / sizeof(unsigned long long));
             if (e == hipSuccess) e = hipMemcpyAsync(h.data(), pt.trace, tbytes, hipMemcpyDeviceToHost, st);
@@ -829,7 +869,7 @@ extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, 
     const bool any_temporal = video && (nframes > 1 || (z0 & 1));
     if (any_temporal && family != 0) return LFM_HIP_ENOTINV;  // ((I - pred) + P) >> 1 drops a bit
     if (video && (z0 & 1) && !d_prev) return LFM_HIP_EINVAL;
-    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, nullptr};
+    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, nullptr, lfm::kSpinLimit, nullptr};
     // without video every frame is spatial: one launch; with video the
     // spatial (even global z) frames first, then the temporal ones on their
     // decoded predecessors

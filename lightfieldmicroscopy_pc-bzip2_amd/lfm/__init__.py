@@ -35,7 +35,7 @@ EXPORTS = [
     # lfm_api.h
     "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
-    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_set_devices", "lfm_get_devices",
+    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_set_devices", "lfm_get_devices", "lfm_default_devices",
     "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab", "lfm_encoder_submit",
     "lfm_encoder_submit_select", "lfm_encoder_wait",
     # lfm_hip.h
@@ -118,6 +118,7 @@ def lib():
                                  ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]
     L.lfm_set_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.lfm_get_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.lfm_default_devices.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.lfm_release_encoders.argtypes = []
     L.lfm_release_encoders.restype = None
     L.lfm_merge_slabs.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
@@ -166,8 +167,7 @@ def require_gpu():
 
 def set_devices(devices=None):
     """Devices the writers farm block ranges to (lfm_set_devices); None or []
-    restores the default (env LFM_GPUS, else the current device inside a
-    WORLD_SIZE > 1 job, else every visible device)."""
+    restores the default (see default_devices)."""
     devices = list(devices or [])
     arr = (ctypes.c_int * max(1, len(devices)))(*devices)
     _check(lib().lfm_set_devices(arr, len(devices)), "lfm_set_devices")
@@ -176,6 +176,15 @@ def set_devices(devices=None):
 def get_devices():
     arr = (ctypes.c_int * 256)()
     n = lib().lfm_get_devices(arr, 256)
+    return list(arr[:min(n, 256)])
+
+
+def default_devices(n_visible, current=-1):
+    """The writers' default device list on a machine with n_visible devices
+    (lfm_default_devices: env LFM_GPUS / LOCAL_WORLD_SIZE / LOCAL_RANK / ...;
+    no device call)."""
+    arr = (ctypes.c_int * 256)()
+    n = lib().lfm_default_devices(int(n_visible), int(current), arr, 256)
     return list(arr[:min(n, 256)])
 
 

@@ -686,6 +686,33 @@ def test_decode_path_switches(lfmlib, oracle, gpu, tmp_path, env):
     assert np.array_equal(np.load(out).reshape(img.shape), img), env
 
 
+@pytest.mark.parametrize("fallback", [True, False])
+def test_unpredict_band_timeout_is_reported(lfmlib, oracle, gpu, tmp_path, fallback):
+    """A band of the cross-CU inverse predictor (band5) that gives up waiting
+    for the band above (here forced: one poll, LFM_UNPREDICT_SPIN=1) sets the
+    launch's error word: the launcher re-runs the frames through band4 and the
+    pixels are exact, or with LFM_UNPREDICT_FALLBACK=0 the read fails -- never
+    wrong pixels returned as success."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    img = oracle.synthetic_lf(256, 192, Z=16, T=13, seed=6)
+    lfmlib.set_family("tiles")
+    p = tmp_path / "to.lfm"
+    lfmlib.write_lfm(str(p), img, predictor_request=8 + 4, nnum=13, video=1)
+    out = tmp_path / "out.npy"
+    code = ("import sys; sys.path.insert(0, %r); import numpy as np, lfm; lfm.set_family('tiles'); "
+            "o, _, _ = lfm.read_lfm(%r); np.save(%r, o)" % (PKG, str(p), str(out)))
+    child_env = dict(os.environ, LFM_UNPREDICT_SPIN="1", LFM_UNPREDICT_FALLBACK="1" if fallback else "0")
+    r = subprocess.run([sys.executable, "-c", code], env=child_env, capture_output=True, text=True, timeout=110)
+    assert "hand-over timed out" in r.stderr, r.stderr[-2000:]
+    if fallback:
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert np.array_equal(np.load(out).reshape(img.shape), img)
+    else:
+        assert r.returncode != 0 and not out.exists()
+
+
 def test_decode_threads_release_device_memory(lfmlib, oracle, gpu, tmp_path):
     """Decodes from short-lived host threads free their per-thread device
     buffers and pinned staging when the thread exits: the

@@ -99,27 +99,31 @@ def test_write_klb_stack_uses_lfm_gpus(lfmlib, oracle, gpu, tmp_path, monkeypatc
     assert p.read_bytes() == oracle.encode(img, header_version=0, nnum=13, family="tiles")
 
 
+@pytest.mark.timeout(420)
 def test_bench_two_ranks_one_shared_lfm(gpu, tmp_path):
-    """bench.py's N-rank path (torchrun, gloo standing in for RCCL, both ranks
-    on device 0, 16 frames per rank): every rank encodes its slab with the
-    product encoder, the slab sizes are all_gathered and every rank places its
-    blocks into one shared .lfm; rank 0 checks it against the oracle's
-    per-layer digests (`verified`)."""
-    import socket
+    """`python bench.py --gpus 2` (no launcher: bench.py starts the two ranks
+    itself, torchrun as a child; gloo stands in for RCCL, both ranks on device
+    0, 16 frames per rank): every rank encodes its slab with the product
+    encoder, the slab sizes are all_gathered and every rank places its blocks
+    into one shared .lfm; rank 0 checks it against the oracle's per-layer
+    digests (`verified`).  Then rank 0 runs the `inproc` leg -- the drop-in
+    writer on config 4 over the N ranks' devices (here two workers on the one
+    GPU) -- while the other rank waits on the host: both encodes give the
+    oracle's cfg4 bytes."""
     import subprocess
     import sys
     from conftest import REPO
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    env = dict(os.environ, LFM_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.join(REPO, "bench.py"), "--gpus", "2",
-           "--frames", "16", "--steps", "2", "--warmup", "1", "--no-decode", "--no-cpu-baseline"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=str(tmp_path))
+    env = dict(os.environ, LFM_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4", LFM_BZ2_GPU_BUDGET_MB="8192")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--frames", "16", "--steps", "2",
+           "--warmup", "1", "--no-decode", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["verified"]["ok"], line
+    legs = line["inproc"]
+    assert legs["gpus_1"]["verified"] is True, legs
+    assert legs["workers_2"]["verified"] is True and legs["workers_2"]["devices"] == [0, 0], legs
 
 
 @pytest.mark.timeout(320)

@@ -8,10 +8,12 @@ the oracle (no GPU); tests/test_multigpu_gpu.py runs the same protocol with
 the product encoder on the GPU."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 
+from conftest import REPO
 from lfm.shard import forced_request, plan_slabs
 
 
@@ -119,3 +121,68 @@ def test_gloo_two_rank_sharded_encode(tmp_path):
     ok, t = res.read_text().split()
     assert ok == "1"
     assert float(t) == pytest.approx(0.5)
+
+
+_LAUNCH_VARS = ("LFM_GPUS", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_SIZE",
+                "OMPI_COMM_WORLD_LOCAL_RANK")
+
+
+@pytest.mark.parametrize("env,nvis,current,want", [
+    ({}, 8, 0, list(range(8))),                                       # plain process: every GPU
+    ({"WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8", "LOCAL_RANK": "3"}, 8, 0, [3]),  # torchrun rank 3
+    ({"WORLD_SIZE": "2", "LOCAL_WORLD_SIZE": "1", "LOCAL_RANK": "0"}, 8, 0, list(range(8))),  # 1 proc per node
+    ({"WORLD_SIZE": "16", "LOCAL_WORLD_SIZE": "8", "LOCAL_RANK": "11"}, 8, 0, [3]),  # modulo visible
+    ({"WORLD_SIZE": "4", "LOCAL_WORLD_SIZE": "4", "LOCAL_RANK": "2"}, 8, 5, [2]),  # rank, not current device
+    ({"WORLD_SIZE": "4"}, 8, 5, [5]),                                 # no local info: current device
+    ({"OMPI_COMM_WORLD_LOCAL_SIZE": "4", "OMPI_COMM_WORLD_LOCAL_RANK": "1"}, 8, 0, [1]),  # MPI launcher
+    ({"OMPI_COMM_WORLD_LOCAL_SIZE": "1", "WORLD_SIZE": "4"}, 4, 0, [0, 1, 2, 3]),
+    ({"LFM_GPUS": "0,0,1", "WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8"}, 2, 0, [0, 0, 1]),  # explicit list wins
+    ({"LFM_GPUS": "3"}, 8, 0, [0, 1, 2]),
+    ({}, 0, -1, []),                                                  # no device
+])
+def test_default_device_policy(lfmlib, monkeypatch, env, nvis, current, want):
+    """The writers' default device list (lfm_default_devices, the policy
+    behind writeImage / writeKLBstack on a node): the number of processes on
+    the node decides, and a rank maps to LOCAL_RANK modulo the visible devices."""
+    for v in _LAUNCH_VARS:
+        monkeypatch.delenv(v, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert lfmlib.default_devices(nvis, current) == want
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_gpus_flag_is_authoritative():
+    """bench.py --gpus N: with no WORLD_SIZE and N > 1 it launches N ranks
+    (torchrun child, 127.0.0.1 rendezvous); under a launcher WORLD_SIZE must
+    equal N; nccl needs N visible devices."""
+    b = _bench()
+    assert b.rank_layout(1, {}, 1) == (1, 0, 0, 1)
+    assert b.rank_layout(8, {}, 8) == (None, 0, 0, 8)
+    assert isinstance(b.rank_layout(8, {}, 1), str)
+    assert b.rank_layout(2, {"LFM_BENCH_BACKEND": "gloo"}, 1) == (None, 0, 0, 2)
+    env = {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2", "LOCAL_WORLD_SIZE": "4"}
+    assert b.rank_layout(4, env, 4) == (4, 2, 2, 4)
+    assert isinstance(b.rank_layout(8, env, 8), str)
+    assert isinstance(b.rank_layout(1, env, 8), str)
+    cmd = b.torchrun_cmd(4, ["--gpus", "4", "--steps", "3"], 29512)
+    assert cmd[cmd.index("-m") + 1] == "torch.distributed.run"
+    assert "--nproc-per-node=4" in cmd and "--master-addr=127.0.0.1" in cmd and "--master-port=29512" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero before any
+    device call (runs on the CPU)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr
