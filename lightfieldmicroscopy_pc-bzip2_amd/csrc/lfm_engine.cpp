@@ -444,7 +444,11 @@ Encoder::Encoder(int device) : device_(device) {}
 Encoder::~Encoder()
 {
     join_inflight();
+    for (UploadPipe& u : up_) u.join();
     if (gpu_ready_) {
+        for (UploadPipe& u : up_)
+            for (hipEvent_t e : u.ev) (void)hipEventDestroy(e);
+        if (up_stream_) (void)hipStreamDestroy(up_stream_);
         (void)hipSetDevice(device_);
         if (d_in_) (void)hipFree(d_in_);
         for (void* d : d_sym_)
@@ -547,12 +551,10 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         return 0;
     };
     const bool pre = gpu_bz && req0 < NUM_PREDICTORS && h.getBytesPerPixel() == 2 && h.Nnum > 0;
-    if (pre && early)
-        if (int rc = select_now()) return rc;
-    fly_[p ^ 1].wait_release();        // the previous encode is in its tail
-    if (trace) ts("released");
-    if (pre && !early)
-        if (int rc = select_now()) return rc;
+    // a host stack starts its chunked upload (and the predictor on the chunks
+    // that have landed) before the previous encode is released: the PCIe
+    // upload runs under the previous encode's GPU bzip2
+    const bool host_early = gpu_bz && upload_pipe_ok(dev, h);
     f.ticket = next_ticket_++;
     f.rc = 0;
     std::memset(&f.st, 0, sizeof(f.st));
@@ -564,6 +566,14 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     }
     if (ticket) *ticket = f.ticket;
     par_ ^= 1;
+    auto fail = [&](int rc) {
+        up_[p].join();
+        f.rc = rc;
+        f.release();
+        return rc;
+    };
+    if (pre && (early || host_early))
+        if (int rc = select_now()) return fail(rc);
     if (pre_k >= 0) {
         f.st.select_ms = pre_ms;
         std::memcpy(f.st.entropy, pre_ent, sizeof(pre_ent));
@@ -577,18 +587,28 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         if (nominal.blockSize[2] == 0) nominal.blockSize[2] = 1;
         level = bzip2_level(nominal);
     }
+    const uint8_t* dsym = nullptr;
+    if (host_early) {
+        if (int rc = normalize_header(h)) return fail(rc);
+        if (int rc = predictor_stage(img, dev, h, nullptr, &dsym, &f.st, slab ? *slab : whole, p)) return fail(rc);
+    }
+    fly_[p ^ 1].wait_release();        // the previous encode is in its tail
+    if (trace) ts("released");
+    if (pre && !early && !host_early) {
+        if (int rc = select_now()) return fail(rc);
+        f.st.select_ms = pre_ms;
+        std::memcpy(f.st.entropy, pre_ent, sizeof(pre_ent));
+    }
     if (!gpu_bz) {  // no GPU bzip2: the whole encode here
         MemSink sink(&mem_ring[p]);
         f.rc = encode_set(img, dev, h, sink, &f.st, threads, slab, p);
         f.release();
         return f.rc;
     }
-    const uint8_t* dsym = nullptr;
-    if ((f.rc = normalize_header(h)) || (f.rc = predictor_stage(img, dev, h, nullptr, &dsym, &f.st, slab ? *slab : whole, p)) ||
-        (f.rc = ensure_gpu())) {
-        f.release();
-        return f.rc;
-    }
+    if (!host_early &&
+        ((f.rc = normalize_header(h)) || (f.rc = predictor_stage(img, dev, h, nullptr, &dsym, &f.st, slab ? *slab : whole, p))))
+        return fail(f.rc);
+    if ((f.rc = ensure_gpu())) return fail(f.rc);
     if (dev && dsym == (const uint8_t*)img) {
         // no predictor stage (forced predictor 0, non-16-bit data): the symbols
         // ARE the caller's image, which the caller may release or refill once
@@ -617,6 +637,15 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         f.st.out_bytes = hh->getCompressedFileSizeInBytes();
         f.release();  // in case the release stage was never reached (host paths)
     });
+    UploadPipe& up = up_[p];
+    if (up.active) {
+        // the caller may release a host stack once submit returns: wait for
+        // its upload (the finisher's GPU bzip2 already runs on the chunks)
+        up.join();
+        f.st.h2d_ms += up.h2d_ms;
+        f.st.predict_ms += up.predict_ms;
+        if (up.rc) return up.rc;  // the finisher's batches fail too; wait() reports it
+    }
     return 0;
 }
 
@@ -670,6 +699,151 @@ void* Encoder::dev_alloc(void*& p, size_t& cap, size_t need)
     if (hipMalloc(&p, need) != hipSuccess) return nullptr;
     cap = need;
     return p;
+}
+
+// ---------------------------------------------------------- upload pipe --
+int Encoder::UploadPipe::wait_frames(uint64_t f_end, hipStream_t st)
+{
+    std::unique_lock<std::mutex> lk(mu);
+    if (!active) return 0;
+    size_t c = (size_t)(std::lower_bound(end.begin(), end.begin() + nchunks, f_end) - end.begin());
+    if (c >= nchunks) c = nchunks - 1;
+    cv.wait(lk, [&] { return recorded > c || rc != 0; });
+    if (rc) return 3;
+    return hipStreamWaitEvent(st, ev[3 * c + 2], 0) == hipSuccess ? 0 : 3;
+}
+
+void Encoder::UploadPipe::join()
+{
+    if (th.joinable()) th.join();
+    std::lock_guard<std::mutex> lk(mu);
+    active = false;
+}
+
+bool Encoder::upload_pipe_ok(bool dev, const klb_image_header& h) const
+{
+    static const bool on = [] {
+        const char* e = std::getenv("LFM_H2D_PIPE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on && !dev && h.getBytesPerPixel() == 2 && h.Nnum > 0;
+}
+
+// Upload the host stack in chunks of whole frames through a ring of device
+// slots and predict each chunk (forced predictor k >= 1) into the set's
+// symbol buffer as it lands (see UploadPipe).  Returns once the uploader
+// thread runs; UploadPipe::join waits for it (the host image is read until
+// then).  The chunk's first frame takes its temporal predecessor from the
+// previous chunk's slot (or the slab's prev frame), which the ring keeps
+// until the chunk after it has been predicted.
+int Encoder::start_upload(const void* img, klb_image_header& h, const SlabSpec& slab, int k, int set)
+{
+    UploadPipe& up = up_[set];
+    up.join();
+    const uint64_t W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
+    const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
+    const size_t fpx = W * H, fs = fpx * 2;
+    const int video = (h.headerVersion >> 7) & 1;
+    static const size_t chunk_target = [] {
+        const char* e = std::getenv("LFM_H2D_CHUNK_MB");
+        const long v = e ? std::atol(e) : 0;
+        return (size_t)(v > 0 ? v : 32) << 20;
+    }();
+    static const size_t ring_target = [] {
+        const char* e = std::getenv("LFM_H2D_RING_MB");
+        const long v = e ? std::atol(e) : 0;
+        return (size_t)(v > 0 ? v : 1024) << 20;
+    }();
+    // >= chunk_target bytes of whole frames; an even count on video stacks
+    // (a spatial and its temporal frame go through the pair kernel together)
+    uint64_t cz = std::max<uint64_t>(1, (chunk_target + fs - 1) / fs);
+    if (video && (cz & 1)) ++cz;
+    cz = std::min<uint64_t>(cz, Z);
+    const uint64_t per_vol = (Z + cz - 1) / cz, nch = V * per_vol;
+    const size_t cbytes = cz * fs;
+    const uint64_t nslot = std::min<uint64_t>(nch, std::max<uint64_t>(2, ring_target / cbytes));
+    if (!dev_alloc(d_in_, d_in_cap_, nslot * cbytes)) return 3;
+    if (!dev_alloc(d_sym_[set], d_sym_cap_[set], V * Z * fs)) return 3;
+    if (!up_stream_ && hipStreamCreateWithFlags(&up_stream_, hipStreamNonBlocking) != hipSuccess) return 3;
+    while (up.ev.size() < 3 * nch) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return 3;
+        up.ev.push_back(e);
+    }
+    const uint16_t* d_prev = nullptr;
+    if (slab.z0 > 0 && video && (slab.z0 & 1)) {
+        if (V != 1 || !slab.prev) return 3;
+        if (!dev_alloc(d_prev_, d_prev_cap_, fs)) return 3;
+        if (hipMemcpyAsync(d_prev_, slab.prev, fs, hipMemcpyHostToDevice, stream_) != hipSuccess) return 3;
+        d_prev = (const uint16_t*)d_prev_;
+    }
+    up.end.assign(nch, 0);
+    for (uint64_t c = 0; c < nch; ++c) up.end[c] = (c / per_vol) * Z + std::min<uint64_t>(Z, (c % per_vol + 1) * cz);
+    {
+        std::lock_guard<std::mutex> lk(up.mu);
+        up.nchunks = nch;
+        up.recorded = 0;
+        up.rc = 0;
+        up.active = true;
+        up.h2d_ms = up.predict_ms = 0.0;
+    }
+    const int fam = current_family(), T = h.Nnum;
+    const uint32_t z0 = slab.z0;
+    uint16_t* const d_in = (uint16_t*)d_in_;
+    uint16_t* const d_sym = (uint16_t*)d_sym_[set];
+    const uint8_t* const src = (const uint8_t*)img;
+    up.th = std::thread([=, &up]() {
+        (void)hipSetDevice(device_);
+        auto t0 = clk::now();
+        int rc = 0;
+        for (uint64_t c = 0; c < nch && !rc; ++c) {
+            const uint64_t v = c / per_vol, za = (c % per_vol) * cz, zb = std::min<uint64_t>(Z, za + cz);
+            uint16_t* slot = d_in + (c % nslot) * cz * fpx;
+            hipEvent_t* e = &up.ev[3 * c];
+            // the slot was chunk c - nslot's; chunk c - nslot + 1 (predicted
+            // after it) also reads that slot's last frame as its temporal prev
+            if (c >= nslot && hipStreamWaitEvent(up_stream_, up.ev[3 * (c - nslot + 1) + 2], 0) != hipSuccess) rc = 3;
+            if (!rc && hipMemcpyAsync(slot, src + (v * Z + za) * fs, (zb - za) * fs, hipMemcpyHostToDevice,
+                                      up_stream_) != hipSuccess)
+                rc = 3;
+            if (!rc && (hipEventRecord(e[0], up_stream_) != hipSuccess ||
+                        hipStreamWaitEvent(stream_, e[0], 0) != hipSuccess))
+                rc = 3;
+            const uint16_t* prev = nullptr;
+            if (video) prev = za > 0 ? d_in + ((c - 1) % nslot) * cz * fpx + (cz - 1) * fpx : d_prev;
+            if (!rc) {
+                (void)hipEventRecord(e[1], stream_);
+                if (lfm_hip_predict(slot, prev, d_sym + (v * Z + za) * fpx, (int)W, (int)H, (int)(zb - za), T, fam, k,
+                                    video, (int)(z0 + za), stream_) != LFM_HIP_OK ||
+                    hipEventRecord(e[2], stream_) != hipSuccess)
+                    rc = 3;
+            }
+            {
+                std::lock_guard<std::mutex> lk(up.mu);
+                if (rc) up.rc = rc;
+                else up.recorded = c + 1;
+            }
+            up.cv.notify_all();
+        }
+        // the host image is no longer read once the copies are done
+        if (hipStreamSynchronize(up_stream_) != hipSuccess) rc = 3;
+        const double h2d = ms_since(t0);
+        double pms = 0.0;
+        if (!rc && hipEventSynchronize(up.ev[3 * (nch - 1) + 2]) == hipSuccess) {
+            for (uint64_t c = 0; c < nch; ++c) {
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, up.ev[3 * c + 1], up.ev[3 * c + 2]) == hipSuccess) pms += ms;
+            }
+        }
+        {
+            std::lock_guard<std::mutex> lk(up.mu);
+            if (rc) up.rc = rc;
+            up.h2d_ms = h2d;
+            up.predict_ms = pms;
+        }
+        up.cv.notify_all();
+    });
+    return 0;
 }
 
 int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym,
@@ -745,6 +919,35 @@ int Encoder::predictor_stage(const void* img, bool dev, klb_image_header& h, con
     (void)hipSetDevice(device_);
     const int fam = current_family();
     const int T = h.Nnum;
+
+    if (keep && upload_pipe_ok(dev, h)) {
+        // host stack, GPU bzip2: chunked upload overlapped with the predictor
+        // and the compression (start_upload); selection first, on frame 0 of
+        // volume (0, 0) or the stack's frame 0 handed in for a slab
+        if (autosel) {
+            auto t0 = clk::now();
+            const void* frame = slab.select_frame ? slab.select_frame : (slab.z0 > 0 ? nullptr : img);
+            if (!frame) return 3;  // a slab's own frame 0 is not the stack's
+            float ent[8];
+            if (int rc = select_host_frame(frame, (int)W, (int)H, T, fam, &k, ent)) return rc;
+            if (st) {
+                st->select_ms += ms_since(t0);
+                std::memcpy(st->entropy, ent, sizeof(ent));
+            }
+        }
+        if (int rc = start_upload(img, h, slab, k, set)) {
+            up_[set].join();
+            return rc;
+        }
+        h.headerVersion = (uint8_t)((hv & 0x80) | k);
+        if (st) st->chosen = k;
+        if (video && fam != 0 && Z > 1)
+            std::fprintf(stderr, "WARNING: video stack with the %s predictor family: the odd frames are coded with the "
+                                 "reference's lossy temporal residual and cannot be decoded exactly\n",
+                         fam == 1 ? "angle" : "space");
+        *dsym = (const uint8_t*)d_sym_;
+        return 0;
+    }
 
     const uint16_t* d_img = (const uint16_t*)img;
     // slab of a larger stack: its first frame may need the raw frame z0 - 1
@@ -951,6 +1154,15 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         int stage;
     };
     HookCtx hctx{fly, release_at};
+    // host stack still uploading (start_upload): a batch waits for the chunks
+    // holding its last block (blocks run x -> y -> z -> c -> t, so that block
+    // reaches furthest into the flattened (t, c, z) frame order)
+    UploadPipe* up = up_[set].active ? &up_[set] : nullptr;
+    auto frames_needed = [&](uint64_t last_block) -> uint64_t {
+        uint64_t o[5], sz[5];
+        g.block(last_block, o, sz);
+        return ((o[4] + sz[4] - 1) * h.xyzct[3] + (o[3] + sz[3] - 1)) * (uint64_t)h.xyzct[2] + o[2] + sz[2];
+    };
     if (fly) {
         std::lock_guard<std::mutex> lk(fly->mu);
         fly->need = (int)std::min<uint64_t>(nslots, nbatch);
@@ -975,6 +1187,12 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             const uint32_t cnt = (uint32_t)std::min<uint64_t>(batch, nblocks - b0);
             sizes[b].assign(cnt, 0);
             flags[b].assign(cnt, 0);
+            if (up && up->wait_frames(frames_needed(b0 + cnt - 1), sl.stream)) {
+                std::lock_guard<std::mutex> lk(mu);
+                state[b] = -1;
+                cv.notify_all();
+                break;
+            }
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
                                           ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
             if (fly && b + nslots >= nbatch) {
@@ -1051,7 +1269,8 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                     // on this batch's own HIP stream: stream_ belongs to the
                     // caller thread's next submit (its predictor stage)
                     hipStream_t fs = bz_[b % nslots].stream;
-                    if (hipMemcpyAsync(h_sym_, d_sym, bytes, hipMemcpyDeviceToHost, fs) != hipSuccess ||
+                    if ((up && up->wait_frames(~0ull, fs)) ||
+                        hipMemcpyAsync(h_sym_, d_sym, bytes, hipMemcpyDeviceToHost, fs) != hipSuccess ||
                         hipStreamSynchronize(fs) != hipSuccess) {
                         rc = 3;
                         break;
@@ -1172,8 +1391,20 @@ int Encoder::encode_set(const void* img, bool dev, klb_image_header& h, Sink& si
     if (rc) return rc;
     auto tc = clk::now();
     if (gpu_bz) {
-        if ((rc = ensure_gpu())) return rc;
+        if ((rc = ensure_gpu())) {
+            up_[set].join();
+            return rc;
+        }
         rc = gpu_compress(dsym, h, sink, st, level, set, nullptr);
+        UploadPipe& up = up_[set];
+        if (up.active) {  // the host image is read until the uploader is done
+            up.join();
+            if (!rc) rc = up.rc;
+            if (st) {
+                st->h2d_ms += up.h2d_ms;
+                st->predict_ms += up.predict_ms;
+            }
+        }
     } else {
         rc = compress_blocks(sym, h, sink, threads, level);
     }

@@ -170,6 +170,29 @@ private:
         void wait_release();
         void reach();         // one last-round batch passed the release stage
     };
+    // Host stacks for the GPU bzip2 path go up in chunks of whole frames on
+    // up_stream_ (one uploader thread per encode), each chunk predicted on
+    // stream_ as soon as it has landed; the GPU bzip2 batches wait (event)
+    // only for the chunks that hold their blocks, so the PCIe upload overlaps
+    // the compression of the layers already predicted.  Chunks pass through a
+    // ring of device slots (LFM_H2D_RING_MB), so the stack's size is not
+    // bounded by it.  LFM_H2D_PIPE=0: the whole volume is uploaded first.
+    struct UploadPipe {
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv;
+        std::vector<hipEvent_t> ev;  // pool: 2 per chunk (predict start / end), kept between encodes
+        std::vector<uint64_t> end;   // per chunk: flattened frame index (v * Z + z) past its last frame
+        size_t nchunks = 0, recorded = 0;  // chunks whose "predicted" event is recorded
+        int rc = 0;
+        bool active = false;
+        double h2d_ms = 0.0, predict_ms = 0.0;
+        // make `st` wait until frames [0, f_end) are predicted (0 or 3)
+        int wait_frames(uint64_t f_end, hipStream_t st);
+        void join();
+    };
+    int start_upload(const void* img, klb_image_header& h, const SlabSpec& slab, int k, int set);
+    bool upload_pipe_ok(bool dev, const klb_image_header& h) const;
     int predictor_stage(const void* img, bool dev, klb_image_header& h, const uint8_t** sym, const uint8_t** dsym,
                         lfm_encode_stats* st, const SlabSpec& slab, int set);
     int gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink, lfm_encode_stats* st, int level, int set,
@@ -181,6 +204,8 @@ private:
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     void join_inflight();
     Inflight fly_[2];                         // by buffer set
+    UploadPipe up_[2];                        // by buffer set
+    hipStream_t up_stream_ = nullptr;         // host -> device chunk copies
     uint64_t next_ticket_ = 1;
     int par_ = 0;                             // buffer set of the next submit
     hipStream_t copy_stream_ = nullptr;       // payload copies the SDMA path cannot take

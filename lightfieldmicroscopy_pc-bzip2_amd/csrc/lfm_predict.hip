@@ -942,6 +942,163 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_vec(FrameSet p, int row
                                                       lane);
 }
 
+// ---- video volumes: frame pairs.  With the video bit, frame z is temporal
+// when z0 + z is odd and its residual needs the RAW previous frame z - 1,
+// which is the volume's own input: predict_vec reads it a second time (a
+// third ring of P rows per temporal item: 6 B per temporal pixel).  A pair
+// item codes the spatial frame z - 1 AND the temporal frame z of one (row
+// piece, strip): the loader streams both frames' rows into two rings (A: frame
+// z - 1, B: frame z), compute waves 0 .. NCW/2 - 1 code frame A, the others
+// frame B, and a B wave takes its P pixels from ring A's row y, which is
+// already there for frame A.  Every input pixel is read once: 4 B per pixel
+// for the whole volume.
+template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
+__device__ __forceinline__ void vec_pair_item(const FrameSet& p, uint16_t* ringA, uint16_t* ringB, int R,
+                                              const uint16_t* fA, const uint16_t* fB, uint16_t* outA, uint16_t* outB,
+                                              int xs, int ys, int ye, int wave, int lane)
+{
+    constexpr int SW = WPR * 512;
+    constexpr int NCWF = NCW / 2;   // compute waves per frame
+    constexpr int RG = NCWF / WPR;  // rows of each frame computed side by side
+    constexpr int RS = RG * RPW;    // rows of each frame per step
+    constexpr int kLoadsPerStep = 2 * RS * (WPR + 1);
+    constexpr int kWait = kLoadsPerStep * (PD - 1) < 63 ? kLoadsPerStep * (PD - 1) : 63;
+    static_assert(NCW % 2 == 0 && NCWF % WPR == 0, "compute waves per frame and row");
+    constexpr int slot = kVHalo + SW;
+    const bool loader = wave == NCW;
+    const int nsteps = (ye - ys + RS - 1) / RS;
+    auto adv = [](int v, int d, int m) { v += d; while (v >= m) v -= m; return v; };
+    auto wrap = [&](int s) { return s < 0 ? s + R : s; };
+    const bool onB = wave >= NCWF;  // wave-uniform
+    const int w = onB ? wave - NCWF : wave;
+    const int rg = w / WPR, sub = w - (w / WPR) * WPR;
+    const int xl = sub * 512 + lane * 8;
+    const int x0 = xs + xl;
+    const bool lane_in = x0 < p.W;
+    const bool full = xs + SW <= p.W;
+    uint16_t* ring = onB ? ringB : ringA;
+    uint16_t* outf = onB ? outB : outA;
+    uint32_t u0bits = 0;
+    int y = ys + rg, sy = 0, vy = 0, lslot = 0;
+    if (!loader) {
+        const int u0 = x0 % T;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u0bits |= (uint32_t)(((u0 + j) % T) == 0) << j;
+        sy = y % R;
+        vy = y % T;
+    } else {
+        const int r0 = max(0, ys - T - 1);
+        int ps = r0 % R;
+        for (int row = r0; row < ys; ++row) {
+            vdma_row<WPR>(ringA, ps, fA, p.W, row, xs, lane);
+            vdma_row<WPR>(ringB, ps, fB, p.W, row, xs, lane);
+            ps = ps + 1 == R ? 0 : ps + 1;
+        }
+        int slot0 = ys % R;
+        for (int s = 0; s < PD && s < nsteps; ++s) {
+#pragma unroll
+            for (int i = 0; i < RS; ++i) {
+                const int src = min(ys + s * RS + i, ye - 1);
+                const int si = adv(slot0, i, R);
+                vdma_row<WPR>(ringA, si, fA, p.W, src, xs, lane);
+                vdma_row<WPR>(ringB, si, fB, p.W, src, xs, lane);
+            }
+            slot0 = adv(slot0, RS, R);
+        }
+        lslot = slot0;
+    }
+    for (int s = 0; s < nsteps; ++s) {
+        if (loader) {
+            if (s + PD < nsteps) wait_vmcnt<kWait>();
+            else wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if (loader) {
+            if (s + PD < nsteps) {
+#pragma unroll
+                for (int i = 0; i < RS; ++i) {
+                    const int src = min(ys + (s + PD) * RS + i, ye - 1);
+                    const int si = adv(lslot, i, R);
+                    vdma_row<WPR>(ringA, si, fA, p.W, src, xs, lane);
+                    vdma_row<WPR>(ringB, si, fB, p.W, src, xs, lane);
+                }
+                lslot = adv(lslot, RS, R);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                if (y < ye && lane_in) {
+                    const int h = kVHalo + xl;
+                    VecRows rw;
+                    load_win(ring + sy * slot + h, rw.r0);
+                    load_win(ring + wrap(sy - 1) * slot + h, rw.r1);
+                    load_win(ring + wrap(sy - T) * slot + h, rw.rT);
+                    load_win(ring + wrap(sy - T - 1) * slot + h, rw.rT1);
+                    v4u o;
+                    if (onB) {  // temporal: P = frame A's raw pixels of this row
+                        const v4u pv = *(const v4u*)(ringA + sy * slot + h);
+                        rw.p[0] = pv.x; rw.p[1] = pv.y; rw.p[2] = pv.z; rw.p[3] = pv.w;
+                        if (y < T || !full) o = vec_slow_row<FAM, K, T, true>(rw, x0, y / T, vy);
+                        else if (x0 < 512)
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, true, true, true>(rw, u0bits, x0)
+                                        : vec_fast_row<FAM, K, T, true, false, true>(rw, u0bits, x0);
+                        else
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, true, true, false>(rw, u0bits, x0)
+                                        : vec_fast_row<FAM, K, T, true, false, false>(rw, u0bits, x0);
+                    } else {
+                        if (y < T || !full) o = vec_slow_row<FAM, K, T, false>(rw, x0, y / T, vy);
+                        else if (x0 < 512)
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, false, true, true>(rw, u0bits, x0)
+                                        : vec_fast_row<FAM, K, T, false, false, true>(rw, u0bits, x0);
+                        else
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, false, true, false>(rw, u0bits, x0)
+                                        : vec_fast_row<FAM, K, T, false, false, false>(rw, u0bits, x0);
+                    }
+                    __builtin_nontemporal_store(o, (v4u*)(outf + (size_t)y * p.W + x0));
+                }
+                y += RG;
+                sy = adv(sy, RG, R);
+                vy = adv(vy, RG, T);
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+// pair u codes frames first + 2u (spatial) and first + 2u + 1 (temporal)
+template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
+__global__ __launch_bounds__(NCW * 64 + 64) void predict_vec_pair(FrameSet p, int rows_per_piece, int npiece,
+                                                                  int nstrip, int xcd_map, int R, int first)
+{
+    extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+    uint16_t* ringA = lds;
+    uint16_t* ringB = lds + R * (kVHalo + WPR * 512);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const size_t fs = (size_t)p.W * p.H;
+    const int b = blockIdx.x;
+    int strip, group;
+    if (xcd_map) {
+        const int q = b >> 3;
+        strip = q % nstrip;
+        group = (q / nstrip) * 8 + (b & 7);
+    } else {
+        strip = b % nstrip;
+        group = b / nstrip;
+    }
+    const int piece = group % npiece;
+    const int fzA = first + 2 * (group / npiece);
+    if (fzA + 1 >= p.nz) return;
+    const int xs = strip * WPR * 512;
+    const int ys = piece * rows_per_piece;
+    const int ye = min(ys + rows_per_piece, p.H);
+    if (ys >= ye) return;
+    vec_pair_item<FAM, K, T, WPR, NCW, RPW, PD>(p, ringA, ringB, R, p.in + (size_t)fzA * fs,
+                                                p.in + (size_t)(fzA + 1) * fs, p.out + (size_t)fzA * fs,
+                                                p.out + (size_t)(fzA + 1) * fs, xs, ys, ye, wave, lane);
+}
+
 // -------------------------------------------------------------- launchers --
 // NCW compute waves + 1 loader wave per workgroup; PD steps of NCW*RPW rows in
 // flight.  Ring rows live during a step: y-T-1 .. y+NCW*RPW-1 plus the PD
@@ -968,14 +1125,15 @@ struct Plan {
 // (1.5 % at 2048 rows / 3 pieces vs 6 % for 256-row segments).  Pieces stay
 // >= 2(T+1) rows.
 // rs = rows per step, sw = strip width (pixels), halo = left halo pixels per slot
+// rings = haloed row rings per workgroup (2 for the frame-pair kernel)
 static hipError_t make_plan_shape(const FrameSet& p, const void* fn, int threads, int rs, int pd, int sw, int halo,
-                                  int copies, Plan& pl)
+                                  int copies, Plan& pl, int rings = 1)
 {
     const bool any_temporal = p.video && (p.nz > 1 || (p.z0 & 1));
     pl.R = rs * (pd + 1) + p.T + 1;
     pl.RP = any_temporal ? rs * (pd + 1) : 0;
     pl.halo = halo;
-    pl.lds = ((size_t)pl.R * (pl.halo + sw) + (size_t)pl.RP * sw) * sizeof(uint16_t);
+    pl.lds = ((size_t)rings * pl.R * (pl.halo + sw) + (size_t)pl.RP * sw) * sizeof(uint16_t);
     pl.nstrip = (p.W + sw - 1) / sw;
     const int ncw = rs;  // rows are padded to whole steps below
     int occ = 0;
@@ -1053,11 +1211,79 @@ static hipError_t launch_vec_shape(const FrameSet& p, hipStream_t st)
     return launch_plan(fn, p, pl, NCW, 1, st);
 }
 
+// frame-pair shape (video volumes): NCW compute waves, NCW / 2 per frame
+template <int FAM>
+struct PairShape {
+    static constexpr int WPR = 1;
+    static constexpr int NCW = 8;
+    static constexpr int RPW = 1;
+    static constexpr int PD = 3;
+};
+
+// A video volume: its (spatial, temporal) frame pairs in one predict_vec_pair
+// launch; a temporal frame 0 (z0 odd: its previous frame is p.prev) and an
+// unpaired last spatial frame go through predict_vec on their own.
+template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
+static hipError_t launch_vec_pairs(const FrameSet& p, hipStream_t st)
+{
+    const size_t fs = (size_t)p.W * p.H;
+    const int first = (p.z0 & 1) ? 1 : 0;
+    const int npairs = (p.nz - first) / 2;
+    using S = VecShape<FAM>;
+    auto single = [&](int fz) -> hipError_t {
+        FrameSet q = p;
+        q.in = p.in + (size_t)fz * fs;
+        q.out = p.out + (size_t)fz * fs;
+        q.prev = fz ? p.in + (size_t)(fz - 1) * fs : p.prev;
+        q.nz = 1;
+        q.z0 = p.z0 + fz;
+        return launch_vec_shape<FAM, K, T, S::WPR, S::NCW, S::RPW, S::PD>(q, st);
+    };
+    if (first) {
+        if (hipError_t e = single(0)) return e;
+    }
+    if (npairs > 0) {
+        const void* fn = (const void*)predict_vec_pair<FAM, K, T, WPR, NCW, RPW, PD>;
+        FrameSet q = p;
+        q.nz = npairs;  // planning unit: a pair
+        q.video = 0;    // no P ring: frame A's ring holds the previous frame
+        Plan pl;
+        hipError_t e = make_plan_shape(q, fn, NCW * 64 + 64, (NCW / 2 / WPR) * RPW, PD, WPR * 512, kVHalo, 1, pl, 2);
+        if (e != hipSuccess) return e;
+        FrameSet a = p;
+        a.halo = pl.halo;
+        int a_rows = pl.rows_per_piece, a_np = pl.npiece, a_nstrip = pl.nstrip, a_x = pl.xcd_map, a_R = pl.R,
+            a_first = first;
+        void* args[] = {(void*)&a, (void*)&a_rows, (void*)&a_np, (void*)&a_nstrip, (void*)&a_x, (void*)&a_R,
+                        (void*)&a_first};
+        e = hipLaunchKernel(fn, dim3(pl.grid), dim3(NCW * 64 + 64), args, pl.lds, st);
+        if (e != hipSuccess) return e;
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (first + 2 * npairs < p.nz) return single(p.nz - 1);
+    return hipSuccess;
+}
+
+static bool pairs_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("LFM_PRED_PAIRS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 template <int FAM, int K>
 static hipError_t launch_vec(const FrameSet& p, hipStream_t st)
 {
     using S = VecShape<FAM>;
-    if (p.T == 15) return launch_vec_shape<FAM, K, 15, S::WPR, S::NCW, S::RPW, S::PD>(p, st);
+    using PS = PairShape<FAM>;
+    const bool pairs = p.video && p.nz >= 2 && pairs_enabled();
+    if (p.T == 15) {
+        if (pairs) return launch_vec_pairs<FAM, K, 15, PS::WPR, PS::NCW, PS::RPW, PS::PD>(p, st);
+        return launch_vec_shape<FAM, K, 15, S::WPR, S::NCW, S::RPW, S::PD>(p, st);
+    }
+    if (pairs) return launch_vec_pairs<FAM, K, 13, PS::WPR, PS::NCW, PS::RPW, PS::PD>(p, st);
     return launch_vec_shape<FAM, K, 13, S::WPR, S::NCW, S::RPW, S::PD>(p, st);
 }
 
@@ -1112,6 +1338,10 @@ static hipError_t launch_fam(int k, const FrameSet& p, hipStream_t st, int force
 
 } // namespace lfm
 
+// probes (scripts/*_probe.hip) include this file for its kernels and
+// launchers only: LFM_PREDICT_NO_ENTRY drops the C entry points below, which
+// instantiate every kernel
+#ifndef LFM_PREDICT_NO_ENTRY
 extern "C" int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
                                int nframes, int T, int family, int predictor, int video_bit, int z0,
                                void* stream_)
@@ -1158,3 +1388,4 @@ extern "C" int lfm_hip_predict_candidates(const uint16_t* d_frame, uint16_t* d_o
     }
     return e == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
 }
+#endif

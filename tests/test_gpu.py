@@ -105,6 +105,26 @@ def test_predict_z0_offset_and_prev(lfmlib, oracle, gpu):
     assert np.array_equal(got, full[3:])
 
 
+@pytest.mark.parametrize("W,H,T,Z,z0", [(1032, 200, 15, 5, 0), (520, 160, 13, 2, 1), (2048, 96, 13, 3, 1),
+                                        (776, 130, 15, 1, 1), (1024, 90, 13, 6, 2)])
+def test_video_frame_pairs_vs_oracle(lfmlib, oracle, gpu, W, H, T, Z, z0):
+    """Video volumes code each (spatial, temporal) frame pair in one work item
+    (predict_vec_pair: the temporal frame's previous frame comes from the
+    spatial frame's ring); a temporal first frame (odd z0, previous frame from
+    d_prev) and an unpaired last frame run alone.  Every family and
+    predictor, partial last strips, full-range frames for the int16 wrap."""
+    torch = gpu
+    full = oracle.synthetic_lf(W, H, Z=Z + z0, T=T, seed=W + 5 * Z + z0)[0, 0]
+    full[-1] = np.random.default_rng(W).integers(0, 65536, size=(H, W), dtype=np.uint16)
+    stack = full[z0:]
+    prev = full[z0 - 1:z0] if z0 else None
+    for fam in FAMS:
+        for k in range(1, 8):
+            got = run_predict(lfmlib, torch, stack, T, fam, k, 1, z0=z0, prev=prev)
+            exp = oracle.predict_volume(full, T, fam, k, 1)[z0:]
+            assert np.array_equal(got, exp), (fam, k)
+
+
 def test_predictor0_is_copy(lfmlib, oracle, gpu):
     torch = gpu
     stack = oracle.synthetic_lf(96, 40, Z=2, T=13)[0, 0]
