@@ -586,6 +586,19 @@ __device__ __forceinline__ uint32_t bucket_put(const BktPart& p, uint32_t n, uin
     return m;
 }
 
+// LDS slot of bucket `key` (BITS bits: the first byte, then the top BITS - 8
+// bits of the second).  A dword's bank is its index mod 32, i.e. the key's
+// low bits -- the top bits of the SECOND byte, which on 16-bit little-endian
+// symbols is the high byte (mostly 0) for every other rotation: half the
+// lanes of an atomic landed on one bank with different addresses.  XOR-ing
+// the low 5 bits with the first byte spreads them (a bijection; every access
+// to the histogram goes through it).
+template <uint32_t BITS>
+__device__ __forceinline__ uint32_t bkt_slot(uint32_t key)
+{
+    return key ^ ((key >> (BITS - 8)) & 31u);
+}
+
 template <uint32_t BITS>
 __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists L)
 {
@@ -614,14 +627,14 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         nx = bucket_fetch(T, n, i0 + kBktTile);
         const uint32_t m = bucket_put(cur, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads)
-            atomicAdd(&hist[((uint32_t)tile[1 + k] << (BITS - 8)) | (tile[2 + k] >> (16 - BITS))], 1u);
+            atomicAdd(&hist[bkt_slot<BITS>(((uint32_t)tile[1 + k] << (BITS - 8)) | (tile[2 + k] >> (16 - BITS)))], 1u);
         __syncthreads();
     }
     // exclusive scan of the buckets; chunk cuts at bucket ends
     constexpr uint32_t per = kBuckets / kBucketThreads;
     static_assert(per <= (1u << (BITS - 8)), "a thread's buckets share their first byte");
     uint32_t sum = 0;
-    for (uint32_t q = 0; q < per; ++q) sum += hist[t * per + q];
+    for (uint32_t q = 0; q < per; ++q) sum += hist[bkt_slot<BITS>(t * per + q)];
     if (sum) {  // every byte of the text starts a rotation: byte c is present iff its buckets are not empty
         const uint32_t c = (t * per) >> (BITS - 8);
         atomicOr(&sinuse[c >> 5], 1u << (c & 31));
@@ -641,7 +654,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     auto cuts_of = [&](auto&& emit) {
         uint32_t off = my0;
         for (uint32_t q = 0; q < per; ++q) {
-            const uint32_t c = hist[t * per + q];
+            const uint32_t c = hist[bkt_slot<BITS>(t * per + q)];
             if (c) {
                 const uint32_t e = off + c;
                 if (c > kChunk) {
@@ -680,8 +693,8 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     {
         uint32_t off = my0;
         for (uint32_t q = 0; q < per; ++q) {
-            const uint32_t c = hist[t * per + q];
-            hist[t * per + q] = off;
+            const uint32_t c = hist[bkt_slot<BITS>(t * per + q)];
+            hist[bkt_slot<BITS>(t * per + q)] = off;
             off += c;
         }
     }
@@ -714,7 +727,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         const uint32_t m = bucket_put(cur, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads) {
             const uint8_t* p = tile + 1 + k;
-            const uint32_t pos = atomicAdd(&hist[((uint32_t)p[0] << (BITS - 8)) | (p[1] >> (16 - BITS))], 1u);
+            const uint32_t pos = atomicAdd(&hist[bkt_slot<BITS>(((uint32_t)p[0] << (BITS - 8)) | (p[1] >> (16 - BITS)))], 1u);
             B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
         }
         __syncthreads();
