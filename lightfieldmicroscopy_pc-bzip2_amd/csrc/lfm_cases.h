@@ -75,9 +75,24 @@ __host__ __device__ constexpr bool temporal_twice(int fam, int k, int tc, int uc
            (fam == 2 && k == 6 && tc == TC_00 && uc == UC_ROW);
 }
 
-// Evaluate formula F with a neighbour accessor g (g.template at<NB_x>()).
+// Every formula is an inner integer expression followed by an arithmetic
+// right shift by formula_shift(F) (0, 1 or 2).  The kernels select between
+// two cases' inner sums when their shifts (and temporal finishing, below)
+// agree, and shift once.
+__host__ __device__ constexpr int formula_shift(int F)
+{
+    return (F >= F_AVG_A_AP && F <= F_AVG_BP_AP) || F == F_P4_0Y || F == F_P4_X0 || F == F_P4_COL ||
+                   F == F_P4_ROW || F == F_P4_IN || F == F_P5_00Q || F == F_P5_0Y || F == F_P5_X0 || F == F_P5_COL ||
+                   F == F_P5_ROW || F == F_P5_IN || F == F_P6_0Y || F == F_P6_X0 || F == F_P6_COL || F == F_P6_ROW ||
+                   F == F_P6_IN
+               ? 1
+               : (F == F_P7_0Y || F == F_P7_X0 || F == F_P7_IN) ? 2 : 0;
+}
+
+// The inner expression of formula F with a neighbour accessor g
+// (g.template at<NB_x>()); eval_formula = eval_inner >> formula_shift.
 template <int F, class G>
-__host__ __device__ __forceinline__ int eval_formula(G& g)
+__host__ __device__ __forceinline__ int eval_inner(G& g)
 {
 #define A (g.template at<NB_A>())
 #define B (g.template at<NB_B>())
@@ -96,45 +111,45 @@ __host__ __device__ __forceinline__ int eval_formula(G& g)
     if constexpr (F == F_AP) return Ap;
     if constexpr (F == F_BP) return Bp;
     if constexpr (F == F_CP) return Cp;
-    if constexpr (F == F_AVG_A_AP) return (A + Ap) >> 1;
-    if constexpr (F == F_AVG_B_BP) return (B + Bp) >> 1;
-    if constexpr (F == F_AVG_A_BP) return (A + Bp) >> 1;
-    if constexpr (F == F_AVG_C_BP) return (C + Bp) >> 1;
-    if constexpr (F == F_AVG_B_AP) return (B + Ap) >> 1;
-    if constexpr (F == F_AVG_C_AP) return (C + Ap) >> 1;
-    if constexpr (F == F_AVG_B_CP) return (B + Cp) >> 1;
-    if constexpr (F == F_AVG_A_CP) return (A + Cp) >> 1;
-    if constexpr (F == F_AVG_C_CP) return (C + Cp) >> 1;
-    if constexpr (F == F_AVG_A_B) return (A + B) >> 1;
-    if constexpr (F == F_AVG_B_A) return (B + A) >> 1;
-    if constexpr (F == F_AVG_BP_AP) return (Bp + Ap) >> 1;
+    if constexpr (F == F_AVG_A_AP) return A + Ap;
+    if constexpr (F == F_AVG_B_BP) return B + Bp;
+    if constexpr (F == F_AVG_A_BP) return A + Bp;
+    if constexpr (F == F_AVG_C_BP) return C + Bp;
+    if constexpr (F == F_AVG_B_AP) return B + Ap;
+    if constexpr (F == F_AVG_C_AP) return C + Ap;
+    if constexpr (F == F_AVG_B_CP) return B + Cp;
+    if constexpr (F == F_AVG_A_CP) return A + Cp;
+    if constexpr (F == F_AVG_C_CP) return C + Cp;
+    if constexpr (F == F_AVG_A_B) return A + B;
+    if constexpr (F == F_AVG_B_A) return B + A;
+    if constexpr (F == F_AVG_BP_AP) return Bp + Ap;
     if constexpr (F == F_ABC) return A + B - C;
     if constexpr (F == F_BAC) return B + A - C;
     if constexpr (F == F_ABC_SUM) return Bp + Ap - Cp;
-    if constexpr (F == F_P4_0Y) return (A + B - C + Bp) >> 1;
-    if constexpr (F == F_P4_X0) return (A + B - C + Ap) >> 1;
-    if constexpr (F == F_P4_COL) return (Bp + Ap - Cp + B) >> 1;
+    if constexpr (F == F_P4_0Y) return A + B - C + Bp;
+    if constexpr (F == F_P4_X0) return A + B - C + Ap;
+    if constexpr (F == F_P4_COL) return Bp + Ap - Cp + B;
     if constexpr (F == F_P4_CORNER) return Bp + Ap - Cp;
-    if constexpr (F == F_P4_ROW) return (Bp + Ap - Cp + A) >> 1;
-    if constexpr (F == F_P4_IN) return (Bp + Ap - Cp + B + A - C) >> 1;
-    if constexpr (F == F_P5_00Q) return (A + (B - C)) >> 1;
-    if constexpr (F == F_P5_0Y) return (A + ((B - C) >> 1) + Bp) >> 1;
-    if constexpr (F == F_P5_X0) return (A + ((B - C) >> 1) + Ap) >> 1;
-    if constexpr (F == F_P5_COL) return (Bp + ((Ap - Cp) >> 1) + B) >> 1;
+    if constexpr (F == F_P4_ROW) return Bp + Ap - Cp + A;
+    if constexpr (F == F_P4_IN) return Bp + Ap - Cp + B + A - C;
+    if constexpr (F == F_P5_00Q) return A + (B - C);
+    if constexpr (F == F_P5_0Y) return A + ((B - C) >> 1) + Bp;
+    if constexpr (F == F_P5_X0) return A + ((B - C) >> 1) + Ap;
+    if constexpr (F == F_P5_COL) return Bp + ((Ap - Cp) >> 1) + B;
     if constexpr (F == F_P5_CORNER) return Bp + ((Ap - Cp) >> 1);
-    if constexpr (F == F_P5_ROW) return (Bp + ((Ap - Cp) >> 1) + A) >> 1;
-    if constexpr (F == F_P5_IN) return (Bp + ((Ap - Cp) >> 1) + B + ((A - C) >> 1)) >> 1;
+    if constexpr (F == F_P5_ROW) return Bp + ((Ap - Cp) >> 1) + A;
+    if constexpr (F == F_P5_IN) return Bp + ((Ap - Cp) >> 1) + B + ((A - C) >> 1);
     if constexpr (F == F_A_HBC) return A + ((B - C) >> 1);
     if constexpr (F == F_B_HAC) return B + ((A - C) >> 1);
-    if constexpr (F == F_P6_0Y) return (B + ((A - C) >> 1) + Bp) >> 1;
-    if constexpr (F == F_P6_X0) return (B + ((A - C) >> 1) + Ap) >> 1;
-    if constexpr (F == F_P6_COL) return (Ap + ((Bp - Cp) >> 1) + B) >> 1;
+    if constexpr (F == F_P6_0Y) return B + ((A - C) >> 1) + Bp;
+    if constexpr (F == F_P6_X0) return B + ((A - C) >> 1) + Ap;
+    if constexpr (F == F_P6_COL) return Ap + ((Bp - Cp) >> 1) + B;
     if constexpr (F == F_P6_CORNER) return Ap + ((Bp - Cp) >> 1);
-    if constexpr (F == F_P6_ROW) return (Ap + ((Bp - Cp) >> 1) + A) >> 1;
-    if constexpr (F == F_P6_IN) return (Ap + ((Bp - Cp) >> 1) + A + ((B - C) >> 1)) >> 1;
-    if constexpr (F == F_P7_0Y) return (A + B + ABp + Bp1) >> 2;
-    if constexpr (F == F_P7_X0) return (A + B + BAp + Ap1) >> 2;
-    if constexpr (F == F_P7_IN) return (Bp1 + Ap1 + B + A) >> 2;
+    if constexpr (F == F_P6_ROW) return Ap + ((Bp - Cp) >> 1) + A;
+    if constexpr (F == F_P6_IN) return Ap + ((Bp - Cp) >> 1) + A + ((B - C) >> 1);
+    if constexpr (F == F_P7_0Y) return A + B + ABp + Bp1;
+    if constexpr (F == F_P7_X0) return A + B + BAp + Ap1;
+    if constexpr (F == F_P7_IN) return Bp1 + Ap1 + B + A;
 #undef A
 #undef B
 #undef C
@@ -146,6 +161,13 @@ __host__ __device__ __forceinline__ int eval_formula(G& g)
 #undef ABp
 #undef BAp
     return 0;
+}
+
+// Evaluate formula F with a neighbour accessor g.
+template <int F, class G>
+__host__ __device__ __forceinline__ int eval_formula(G& g)
+{
+    return eval_inner<F>(g) >> formula_shift(F);
 }
 
 // Residual before the int16 store, for a case (FAM, K, TC, UC).
@@ -171,6 +193,27 @@ __host__ __device__ __forceinline__ int case_residual(G& g, int I, int P)
             return ((I - eval_formula<F>(g)) + P) >> 1;
         }
     }
+}
+
+// How a case turns its prediction into the residual (as case_residual above):
+// 0 spatial I - pred; 1 temporal tiles I - ((pred + P) >> 1); 2 temporal with
+// no prediction I - P; 3 temporal angle / space ((I - pred) + P) >> 1; 4 the
+// same with "+ P >> 1" applied twice.
+__host__ __device__ constexpr int finish_kind(int fam, int k, int tc, int uc, bool temporal)
+{
+    return !temporal ? 0
+                     : case_formula(fam, k, tc, uc) == F_Z ? 2
+                                                          : fam == 0 ? 1 : temporal_twice(fam, k, tc, uc) ? 4 : 3;
+}
+
+template <int KIND>
+__host__ __device__ __forceinline__ int finish_residual(int pred, int I, int P)
+{
+    if constexpr (KIND == 0) return I - pred;
+    if constexpr (KIND == 1) return I - ((pred + P) >> 1);
+    if constexpr (KIND == 2) return I - P;
+    if constexpr (KIND == 3) return ((I - pred) + P) >> 1;
+    return ((((I - pred) + P) >> 1) + P) >> 1;
 }
 
 // zig-zag symbol of the int16-stored residual (lfm_Predictors.cu:16-26)

@@ -436,7 +436,7 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_ring(FrameSet p, int ro
     uint16_t* ring = lds;
     uint16_t* pring = lds + R * (p.halo + kStrip);
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
     const size_t fs = (size_t)p.W * p.H;
     const int b = blockIdx.x;
     int strip, group;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_cands(FrameSet p, int r
 {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
     const int b = blockIdx.x;
     int strip, piece;
     if (xcd_map) {
@@ -569,31 +569,107 @@ struct VecRows {
     }
 };
 
-// pixel J on a row y >= T of a full strip: tile case TC_XY except x < T (TC_0Y,
-// FIRST strip only); position case by (u == 0) per pixel and V0 per row
+// Per-lane bit masks of a work item's lanes, one 64-bit (SGPR pair) mask per
+// pixel J of the lane's 8: u[J] = lanes whose pixel J starts a lens column
+// (u == 0); t[J] = lanes whose pixel J lies in the frame's first lens column
+// (x < T).  Computed once per item by ballots, so a row selects between two
+// case formulas with one v_cndmask per pixel instead of rebuilding a mask.
+struct LaneMasks {
+    uint64_t u[8];
+    uint64_t t[8];
+};
+
+__device__ __forceinline__ LaneMasks lane_masks(uint32_t u0bits, int x0, int T)
+{
+    LaneMasks m;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        m.u[j] = __builtin_amdgcn_ballot_w64(((u0bits >> j) & 1u) != 0);
+        m.t[j] = __builtin_amdgcn_ballot_w64(x0 + j < T);
+    }
+    return m;
+}
+
+// m's bit for this lane ? if_set : if_clear (v_cndmask_b32 with an SGPR-pair mask)
+__device__ __forceinline__ int lane_sel(uint64_t m, int if_set, int if_clear)
+{
+    int r;
+    asm("" : "+s"(m));  // an SGPR pair even where the mask is a known constant
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+    return r;
+}
+
+// residual (32 bits, before the int16 store) of pixel J on a row y >= T of a
+// full strip: tile case TC_XY except x < T (TC_0Y, FIRST strip only);
+// position case by (u == 0) per pixel and V0 per row
 template <int FAM, int K, int T, bool TEMP, bool V0, bool FIRST, int J>
-__device__ __forceinline__ uint32_t vec_fast_px(const VecRows& rw, uint32_t u0bits, int x0)
+__device__ __forceinline__ int vec_fast_res(const VecRows& rw, const LaneMasks& lm, int x0)
 {
     constexpr int ucU = V0 ? UC_CORNER : UC_COL;
     constexpr int ucI = V0 ? UC_ROW : UC_IN;
     VecNb<T, J> g{rw.r0, rw.r1, rw.rT, rw.rT1};
     const int I = rw.r0.template px<16 + J>();
     const int P = TEMP ? rw.template prev<J>() : 0;
-    if constexpr (K == 0) return (uint32_t)(I + P) & 0xFFFFu;  // diagnostic: copy through the ring
-    const int m0 = -(int)((u0bits >> J) & 1u);
+    if constexpr (K == 0) {
+        return I + P;  // diagnostic: copy through the ring
+    } else {
+    constexpr int Fu = case_formula(FAM, K, TC_XY, ucU), Fi = case_formula(FAM, K, TC_XY, ucI);
+    constexpr int Gu = case_formula(FAM, K, TC_0Y, ucU), Gi = case_formula(FAM, K, TC_0Y, ucI);
+    constexpr int kind = finish_kind(FAM, K, TC_XY, ucI, TEMP), sh = formula_shift(Fi);
+    constexpr bool same_xy = finish_kind(FAM, K, TC_XY, ucU, TEMP) == kind && formula_shift(Fu) == sh;
+    constexpr bool same_0y = finish_kind(FAM, K, TC_0Y, ucU, TEMP) == kind && formula_shift(Gu) == sh &&
+                             finish_kind(FAM, K, TC_0Y, ucI, TEMP) == kind && formula_shift(Gi) == sh;
+    constexpr bool kind_xy = finish_kind(FAM, K, TC_XY, ucU, TEMP) == kind;
+    constexpr bool kind_0y = finish_kind(FAM, K, TC_0Y, ucU, TEMP) == kind &&
+                             finish_kind(FAM, K, TC_0Y, ucI, TEMP) == kind;
+    if constexpr (same_xy && (!FIRST || same_0y)) {
+        // one inner sum selected per pixel, one shift, one finish
+        int S = lane_sel(lm.u[J], eval_inner<Fu>(g), eval_inner<Fi>(g));
+        if constexpr (FIRST) {
+            if (x0 < T)  // lanes of the first lens column (uniform per lane)
+                S = lane_sel(lm.t[J], lane_sel(lm.u[J], eval_inner<Gu>(g), eval_inner<Gi>(g)), S);
+        }
+        return finish_residual<kind>(S >> sh, I, P);
+    } else if constexpr (kind_xy && (!FIRST || kind_0y)) {
+        // different shifts: one prediction selected per pixel, one finish
+        int pred = lane_sel(lm.u[J], eval_formula<Fu>(g), eval_formula<Fi>(g));
+        if constexpr (FIRST) {
+            if (x0 < T)
+                pred = lane_sel(lm.t[J], lane_sel(lm.u[J], eval_formula<Gu>(g), eval_formula<Gi>(g)), pred);
+        }
+        return finish_residual<kind>(pred, I, P);
+    }
     const int r_u = case_residual<FAM, K, TC_XY, ucU, TEMP>(g, I, P);
     const int r_i = case_residual<FAM, K, TC_XY, ucI, TEMP>(g, I, P);
-    int res = r_i ^ ((r_u ^ r_i) & m0);
+    int res = lane_sel(lm.u[J], r_u, r_i);
     if constexpr (FIRST) {
         if (x0 < T) {  // lanes of the first lens column (uniform per lane)
-            const int mt = -(int)(x0 + J < T);
             const int t_u = case_residual<FAM, K, TC_0Y, ucU, TEMP>(g, I, P);
             const int t_i = case_residual<FAM, K, TC_0Y, ucI, TEMP>(g, I, P);
-            const int rt = t_i ^ ((t_u ^ t_i) & m0);
-            res = res ^ ((rt ^ res) & mt);
+            res = lane_sel(lm.t[J], lane_sel(lm.u[J], t_u, t_i), res);
         }
     }
-    return zigzag16(res);
+    return res;
+    }
+}
+
+// the residuals of pixels 2M, 2M+1 as one packed pair (v_perm of their low
+// halves) and their zig-zag symbols in packed 16-bit arithmetic
+template <int FAM, int K, int T, bool TEMP, bool V0, bool FIRST, int M>
+__device__ __forceinline__ uint32_t vec_fast_pair(const VecRows& rw, const LaneMasks& lm, int x0)
+{
+    const int r0 = vec_fast_res<FAM, K, T, TEMP, V0, FIRST, 2 * M>(rw, lm, x0);
+    const int r1 = vec_fast_res<FAM, K, T, TEMP, V0, FIRST, 2 * M + 1>(rw, lm, x0);
+    // (inline asm: seen as reading only the low halves, the builtin lets the
+    // compiler narrow the residual arithmetic to 16 bits, where an exact
+    // (a + b) >> 1 costs 4 instructions instead of 2)
+    uint32_t pr;
+    asm("v_perm_b32 %0, %1, %2, %3" : "=v"(pr) : "v"(r1), "v"(r0), "s"(0x05040100u));
+    if constexpr (K == 0) return pr;
+    typedef short s16x2_ __attribute__((ext_vector_type(2)));
+    const s16x2_ v = __builtin_bit_cast(s16x2_, pr);
+    const s16x2_ one{1, 1}, fifteen{15, 15};
+    return __builtin_bit_cast(uint32_t, v << one) ^ __builtin_bit_cast(uint32_t, v >> fifteen);
 }
 
 // any pixel J (rows y < T): full per-pixel case logic
@@ -720,7 +796,7 @@ __device__ __forceinline__ uint32_t vec_pk_pair(const VecRows& rw, uint32_t u0bi
 }
 
 template <int FAM, int K, int T, bool TEMP, bool V0, bool FIRST>
-__device__ __forceinline__ v4u vec_fast_row(const VecRows& rw, uint32_t u0bits, int x0)
+__device__ __forceinline__ v4u vec_fast_row(const VecRows& rw, uint32_t u0bits, const LaneMasks& lm, int x0)
 {
     if constexpr (pk_row_ok<FAM, K, TEMP, V0, FIRST>()) {
         uint32_t firstbits = 0;
@@ -736,14 +812,10 @@ __device__ __forceinline__ v4u vec_fast_row(const VecRows& rw, uint32_t u0bits, 
         return o;
     }
     v4u o;
-    o.x = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 0>(rw, u0bits, x0) |
-          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 1>(rw, u0bits, x0) << 16);
-    o.y = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 2>(rw, u0bits, x0) |
-          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 3>(rw, u0bits, x0) << 16);
-    o.z = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 4>(rw, u0bits, x0) |
-          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 5>(rw, u0bits, x0) << 16);
-    o.w = vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 6>(rw, u0bits, x0) |
-          (vec_fast_px<FAM, K, T, TEMP, V0, FIRST, 7>(rw, u0bits, x0) << 16);
+    o.x = vec_fast_pair<FAM, K, T, TEMP, V0, FIRST, 0>(rw, lm, x0);
+    o.y = vec_fast_pair<FAM, K, T, TEMP, V0, FIRST, 1>(rw, lm, x0);
+    o.z = vec_fast_pair<FAM, K, T, TEMP, V0, FIRST, 2>(rw, lm, x0);
+    o.w = vec_fast_pair<FAM, K, T, TEMP, V0, FIRST, 3>(rw, lm, x0);
     return o;
 }
 
@@ -831,6 +903,7 @@ __device__ __forceinline__ void vec_item(const FrameSet& p, uint16_t* ring, int 
     const bool lane_in = x0 < p.W;
     const bool full = xs + SW <= p.W;
     uint32_t u0bits = 0;
+    LaneMasks lm{};
     int y = ys + rg, sy = 0, py = 0, vy = 0;
     int lslot = 0, lpslot = 0;
     if (!loader) {
@@ -856,6 +929,7 @@ __device__ __forceinline__ void vec_item(const FrameSet& p, uint16_t* ring, int 
         lslot = slot0;
         lpslot = pslot0;
     }
+    lm = lane_masks(u0bits, x0, T);  // every lane of the wave (the loader's are unused)
     for (int s = 0; s < nsteps; ++s) {
         if (loader) {
             if (s + PD < nsteps) wait_vmcnt<kWait>();
@@ -886,11 +960,11 @@ __device__ __forceinline__ void vec_item(const FrameSet& p, uint16_t* ring, int 
                     if (y < T || !full) {
                         o = vec_slow_row<FAM, K, T, TEMP>(rw, x0, y / T, vy);
                     } else if (x0 < 512) {  // the strip that starts the frame: first lens column
-                        o = vy == 0 ? vec_fast_row<FAM, K, T, TEMP, true, true>(rw, u0bits, x0)
-                                    : vec_fast_row<FAM, K, T, TEMP, false, true>(rw, u0bits, x0);
+                        o = vy == 0 ? vec_fast_row<FAM, K, T, TEMP, true, true>(rw, u0bits, lm, x0)
+                                    : vec_fast_row<FAM, K, T, TEMP, false, true>(rw, u0bits, lm, x0);
                     } else {
-                        o = vy == 0 ? vec_fast_row<FAM, K, T, TEMP, true, false>(rw, u0bits, x0)
-                                    : vec_fast_row<FAM, K, T, TEMP, false, false>(rw, u0bits, x0);
+                        o = vy == 0 ? vec_fast_row<FAM, K, T, TEMP, true, false>(rw, u0bits, lm, x0)
+                                    : vec_fast_row<FAM, K, T, TEMP, false, false>(rw, u0bits, lm, x0);
                     }
                     __builtin_nontemporal_store(o, (v4u*)(outf + (size_t)y * p.W + x0));
                 }
@@ -913,7 +987,7 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_vec(FrameSet p, int row
     uint16_t* ring = lds;
     uint16_t* pring = lds + R * (kVHalo + WPR * 512);
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
     const size_t fs = (size_t)p.W * p.H;
     const int b = blockIdx.x;
     int strip, group;
@@ -979,6 +1053,7 @@ __device__ __forceinline__ void vec_pair_item(const FrameSet& p, uint16_t* ringA
     uint16_t* ring = onB ? ringB : ringA;
     uint16_t* outf = onB ? outB : outA;
     uint32_t u0bits = 0;
+    LaneMasks lm{};
     int y = ys + rg, sy = 0, vy = 0, lslot = 0;
     if (!loader) {
         const int u0 = x0 % T;
@@ -1007,6 +1082,7 @@ __device__ __forceinline__ void vec_pair_item(const FrameSet& p, uint16_t* ringA
         }
         lslot = slot0;
     }
+    lm = lane_masks(u0bits, x0, T);  // every lane of the wave (the loader's are unused)
     for (int s = 0; s < nsteps; ++s) {
         if (loader) {
             if (s + PD < nsteps) wait_vmcnt<kWait>();
@@ -1040,19 +1116,19 @@ __device__ __forceinline__ void vec_pair_item(const FrameSet& p, uint16_t* ringA
                         rw.p[0] = pv.x; rw.p[1] = pv.y; rw.p[2] = pv.z; rw.p[3] = pv.w;
                         if (y < T || !full) o = vec_slow_row<FAM, K, T, true>(rw, x0, y / T, vy);
                         else if (x0 < 512)
-                            o = vy == 0 ? vec_fast_row<FAM, K, T, true, true, true>(rw, u0bits, x0)
-                                        : vec_fast_row<FAM, K, T, true, false, true>(rw, u0bits, x0);
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, true, true, true>(rw, u0bits, lm, x0)
+                                        : vec_fast_row<FAM, K, T, true, false, true>(rw, u0bits, lm, x0);
                         else
-                            o = vy == 0 ? vec_fast_row<FAM, K, T, true, true, false>(rw, u0bits, x0)
-                                        : vec_fast_row<FAM, K, T, true, false, false>(rw, u0bits, x0);
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, true, true, false>(rw, u0bits, lm, x0)
+                                        : vec_fast_row<FAM, K, T, true, false, false>(rw, u0bits, lm, x0);
                     } else {
                         if (y < T || !full) o = vec_slow_row<FAM, K, T, false>(rw, x0, y / T, vy);
                         else if (x0 < 512)
-                            o = vy == 0 ? vec_fast_row<FAM, K, T, false, true, true>(rw, u0bits, x0)
-                                        : vec_fast_row<FAM, K, T, false, false, true>(rw, u0bits, x0);
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, false, true, true>(rw, u0bits, lm, x0)
+                                        : vec_fast_row<FAM, K, T, false, false, true>(rw, u0bits, lm, x0);
                         else
-                            o = vy == 0 ? vec_fast_row<FAM, K, T, false, true, false>(rw, u0bits, x0)
-                                        : vec_fast_row<FAM, K, T, false, false, false>(rw, u0bits, x0);
+                            o = vy == 0 ? vec_fast_row<FAM, K, T, false, true, false>(rw, u0bits, lm, x0)
+                                        : vec_fast_row<FAM, K, T, false, false, false>(rw, u0bits, lm, x0);
                     }
                     __builtin_nontemporal_store(o, (v4u*)(outf + (size_t)y * p.W + x0));
                 }
@@ -1075,7 +1151,7 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_vec_pair(FrameSet p, in
     uint16_t* ringA = lds;
     uint16_t* ringB = lds + R * (kVHalo + WPR * 512);
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
     const size_t fs = (size_t)p.W * p.H;
     const int b = blockIdx.x;
     int strip, group;

@@ -17,8 +17,9 @@ __global__ void isa_row(const uint16_t* src, v4u* dst, int x0, uint32_t u0bits)
     load_win(p + 128, rw.rT1);
     const v4u pv = *(const v4u*)(p + 160);
     rw.p[0] = pv.x; rw.p[1] = pv.y; rw.p[2] = pv.z; rw.p[3] = pv.w;
+    const LaneMasks lm = lane_masks(u0bits, x0, T);
     asm volatile("; ROW_BEGIN" ::: "memory");
-    const v4u o = vec_fast_row<FAM, K, T, TEMP, V0, FIRST>(rw, u0bits, x0);
+    const v4u o = vec_fast_row<FAM, K, T, TEMP, V0, FIRST>(rw, u0bits, lm, x0);
     asm volatile("; ROW_END" ::: "memory");
     dst[threadIdx.x] = o;
 }

@@ -121,6 +121,15 @@ int main(int argc, char** argv)
     auto run = [&](const char* name, Shape s, int fam, int k, auto launch) { run_prep(name, s, fam, k, launch, ident); };
     const Shape c3{2048, 2048, 64, 15, 0}, c3v{2048, 2048, 64, 15, 1}, c5{4096, 4096, 32, 13, 1};
     run("tilesP4", c3, 0, 4, [](const FrameSet& p) { return launch_vec<0, 4>(p, 0); });
+#define SHAPE(WPR, NCW, RPW, PD)                                                                             \
+    run("tilesP4_w" #WPR "_c" #NCW "_r" #RPW "_pd" #PD, c3, 0, 4,                                          \
+        [](const FrameSet& p) { return launch_vec_shape<0, 4, 15, WPR, NCW, RPW, PD>(p, 0); });
+    SHAPE(1, 4, 1, 3)
+    SHAPE(1, 8, 1, 3)
+    SHAPE(2, 8, 1, 3)
+    SHAPE(1, 4, 2, 2)
+    SHAPE(2, 4, 1, 3)
+#undef SHAPE
     run("tilesP4_video", c3v, 0, 4, [](const FrameSet& p) { return launch_vec<0, 4>(p, 0); });
     run("tilesP4_c5", c5, 0, 4, [](const FrameSet& p) { return launch_vec<0, 4>(p, 0); });
     using S0v = VecShape<0>;
