@@ -329,6 +329,75 @@ def config5_leg(local, threads, nvol=4):
                     "upload of the payload and download of the pixels included)"}
 
 
+def config5_host_leg(local, threads, nvol):
+    """Config 5 streamed from HOST memory through the drop-in writer and
+    reader: nvol t-volumes of the 4096 x 4096 x 32 video stack (tiles, Nnum
+    13, auto) in one host array -> lfm_encoder_encode_multi (the block
+    scheduler behind klb_imageIO::writeImage; t-volumes farmed over the
+    visible devices, chunked uploads overlapped with the predictor and GPU
+    bzip2) -> one in-memory .lfm; volumes 0..3 SHA-256-checked against the
+    oracle (cfg5x4), then the host input is released and every volume is
+    read back on its own (lfm_decode_memory_roi, readKLBroiInPlace's path)
+    and compared with its regenerated pixels.  Peak RSS is the process's."""
+    import resource
+    X5, Y5, Z5, T5, seed = 4096, 4096, 32, 13, 0x4C464D05
+    e = _manifest("cfg5x4_4096x4096x32x1x4_video_tiles_auto")
+    img = np.empty((nvol, 1, Z5, Y5, X5), dtype=np.uint16)
+    d = torch.empty((Z5, Y5, X5), dtype=torch.int16, device="cuda")
+    for t in range(nvol):
+        lfm.synth_device(d, X5, Y5, Z5, T5, t_index=t, idx0=t * Z5 * X5 * Y5, seed=seed)
+        torch.from_numpy(img[t, 0].view(np.int16)).copy_(d)
+        if t % 10 == 9:
+            print("config5_host: %d / %d volumes generated" % (t + 1, nvol), file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    lfm.set_family("tiles")
+    px = nvol * X5 * Y5 * Z5
+    enc = lfm.Encoder(device=local, num_threads=threads)
+    out = {"workload": "%d t-volumes of config 5 (4096x4096x32x1x%d, video, tiles, Nnum 13, auto) from host memory"
+                       % (nvol, nvol),
+           "path": "lfm_encoder_encode_multi (klb_imageIO::writeImage's scheduler, devices %s) -> in-memory .lfm; "
+                   "per-volume lfm_decode_memory_roi" % lfm.get_devices()}
+    try:
+        t0 = time.perf_counter()
+        b, st = enc.encode_multi(img, header_version=0x80, nnum=T5, copy=False)
+        enc_s = time.perf_counter() - t0
+        print("config5_host: encoded in %.2f s" % enc_s, file=sys.stderr, flush=True)
+        nb = 4 * 43 * 43  # blocks per volume (96 x 96 x 8)
+        offs = np.frombuffer(b, dtype="<u8", count=nvol * nb, offset=320)
+        base, prev, sha_ok = 320 + 8 * nvol * nb, 0, None
+        if e is not None:
+            sha_ok = True
+            for t in range(min(4, nvol)):
+                end = int(offs[(t + 1) * nb - 1])
+                sha_ok = sha_ok and hashlib.sha256(b[base + prev:base + end]).hexdigest() == e["volume_sha256"][t]
+                prev = end
+        lfm_bytes = len(b)
+        del img
+        exact, dec_s = True, 0.0
+        for t in range(nvol):
+            t1 = time.perf_counter()
+            v = lfm.decode_roi(b, [0, 0, 0, 0, t], [X5 - 1, Y5 - 1, Z5 - 1, 0, t], num_threads=threads)
+            dec_s += time.perf_counter() - t1
+            lfm.synth_device(d, X5, Y5, Z5, T5, t_index=t, idx0=t * Z5 * X5 * Y5, seed=seed)
+            exact = exact and bool(np.array_equal(v.reshape(Z5, Y5, X5), d.cpu().numpy().view(np.uint16)))
+            del v
+            if t % 10 == 9:
+                print("config5_host: %d / %d volumes read back" % (t + 1, nvol), file=sys.stderr, flush=True)
+    finally:
+        enc.close()
+        lfm.release_encoders()
+        lfm.set_family(FAMILY)
+    out.update({"volumes": nvol, "encode_Mpixel_per_s": round(px / enc_s / 1e6, 1), "encode_s": round(enc_s, 3),
+                "h2d_ms": round(st["h2d_ms"], 1), "ratio": round(px * 2 / lfm_bytes, 4),
+                "verified": {"against": "cfg5x4 per-volume SHA-256 of volumes 0..%d (oracle, reference bzip2-1.0.6)"
+                                        % (min(4, nvol) - 1), "ok": sha_ok},
+                "decode_Mpixel_per_s": round(px / dec_s / 1e6, 1), "decode_s": round(dec_s, 3),
+                "decode_exact": exact,
+                "peak_rss_GB": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024 / 1e9, 2),
+                "input_GB": round(px * 2 / 1e9, 2), "lfm_GB": round(lfm_bytes / 1e9, 2)})
+    return out
+
+
 def _lfm_manifest(name):
     path = os.path.join(REPO, "tests", "golden", "lfm_manifest.json")
     try:
@@ -493,6 +562,10 @@ def main():
     ap.add_argument("--no-config5", action="store_true")
     ap.add_argument("--no-small", action="store_true")
     ap.add_argument("--no-inproc", action="store_true")
+    ap.add_argument("--config5-host-volumes", type=int, default=8,
+                    help="t-volumes of the config5_host leg (N = 1; 0: skip); the full stack is 100")
+    ap.add_argument("--only-config5-host", action="store_true",
+                    help="skip the timed encode and every other leg (a long config5_host run)")
     args = ap.parse_args()
 
     # device_count() creates no HIP context on this image: safe before the spawn
@@ -524,6 +597,12 @@ def main():
     lfm.set_family(FAMILY)
     zf = args.frames
     threads = host_threads(local_world)
+    if args.only_config5_host:
+        if world > 1 or args.config5_host_volumes < 1:
+            print("bench.py: --only-config5-host runs one process with --config5-host-volumes >= 1", file=sys.stderr)
+            sys.exit(2)
+        print(json.dumps({"config5_host": config5_host_leg(local, threads, args.config5_host_volumes)}), flush=True)
+        return
 
     d_img = torch.empty((zf, Y, X), dtype=torch.int16, device="cuda")
     # rank r holds z-slab r (frames r*zf .. r*zf+zf-1) of a (world * zf)-frame stack
@@ -700,6 +779,8 @@ def main():
         line["configs_1_2"] = small_configs_leg(local, threads)
     if rank == 0 and world == 1 and not args.no_config5:
         line["config5"] = config5_leg(local, threads)
+    if rank == 0 and world == 1 and args.config5_host_volumes > 0:
+        line["config5_host"] = config5_host_leg(local, threads, args.config5_host_volumes)
     if rank == 0 and world == 1 and not args.no_inproc:
         nvis = torch.cuda.device_count()
         legs = [[local]] + ([list(range(nvis))] if nvis > 1 else [])

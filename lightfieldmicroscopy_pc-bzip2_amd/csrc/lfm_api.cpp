@@ -251,3 +251,14 @@ extern "C" int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, in
                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     return rc;
 }
+
+extern "C" int lfm_decode_memory_roi(const uint8_t* buf, uint64_t len, const uint32_t lb[KLB_DATA_DIMS],
+                                     const uint32_t ub[KLB_DATA_DIMS], void* out, int numThreads)
+{
+    if (!buf || !lb || !ub || !out) return 3;
+    klb_image_header h;
+    int rc = h.parseHeader(buf, len);
+    if (rc) return rc;
+    const size_t hs = h.getSizeInBytes();
+    return lfm::decode_roi(buf + hs, len - hs, h, lb, ub, (uint8_t*)out, numThreads, lfm::current_family());
+}

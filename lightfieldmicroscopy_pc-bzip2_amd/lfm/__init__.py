@@ -35,7 +35,7 @@ EXPORTS = [
     # lfm_api.h
     "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
-    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_set_devices", "lfm_get_devices", "lfm_default_devices",
+    "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_decode_memory_roi", "lfm_set_devices", "lfm_get_devices", "lfm_default_devices",
     "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab", "lfm_encoder_submit",
     "lfm_encoder_submit_select", "lfm_encoder_wait",
     # lfm_hip.h
@@ -126,6 +126,7 @@ def lib():
     L.lfm_free.argtypes = [vp]
     L.lfm_free.restype = None
     L.lfm_decode_memory.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_int]
+    L.lfm_decode_memory_roi.argtypes = [vp, ctypes.c_uint64, u32p, u32p, vp, ctypes.c_int]
     L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_unpredict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_predict_candidates.argtypes = [vp, vp] + [ctypes.c_int] * 4 + [vp]
@@ -482,6 +483,16 @@ def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):
         shape_tczyx = (xyzct[4], xyzct[3], xyzct[2], xyzct[1], xyzct[0])
     out = np.empty(shape_tczyx, dtype=dtype)
     _check(lib().lfm_decode_memory(buf, len(buf), out.ctypes.data, num_threads), "lfm_decode_memory")
+    return out
+
+
+def decode_roi(buf, lb, ub, dtype=np.uint16, num_threads=-1):
+    """Region lb .. ub (inclusive, [x, y, z, c, t]) of an in-memory .lfm
+    (lfm_decode_memory_roi); returns an array [t, c, z, y, x] of the region."""
+    shape = tuple(int(u) - int(l) + 1 for l, u in zip(lb, ub))[::-1]
+    out = np.empty(shape, dtype=dtype)
+    _check(lib().lfm_decode_memory_roi(_addr(buf), len(buf), _u32(lb), _u32(ub), out.ctypes.data, num_threads),
+           "lfm_decode_memory_roi")
     return out
 
 
