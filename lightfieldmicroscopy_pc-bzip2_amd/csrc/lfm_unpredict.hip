@@ -854,6 +854,9 @@ static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st)
 
 } // namespace lfm
 
+// (checks that compile this file for one kernel define LFM_UNPREDICT_NO_ENTRY:
+// the entry point below instantiates every kernel)
+#ifndef LFM_UNPREDICT_NO_ENTRY
 extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
                                  int nframes, int T, int family, int predictor, int video_bit, int z0, void* stream_)
 {
@@ -890,3 +893,4 @@ extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, 
     }
     return LFM_HIP_OK;
 }
+#endif

@@ -239,3 +239,29 @@ def test_family_switch(lfmlib):
     lfmlib.set_family("tiles")
     with pytest.raises(lfmlib.LfmError):
         lfmlib.set_family(5)
+
+
+def test_band5_release_wait_covers_the_round_stores():
+    """The inverse predictor's band hand-over publishes progress after a
+    hand-counted `s_waitcnt vmcnt(2)` (3 on temporal frames): compile
+    unpredict_band5 (one predictor per family) to gfx950 assembly and check,
+    on the loop's back edge, that at least that many vector memory
+    instructions follow the second-to-last round's pixel store -- so the wait
+    proves every store but the last round's complete, whatever order the
+    compiler chose (scripts/check_band5_isa.py)."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    import check_band5_isa as C
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        asm = os.path.join(d, "b5.s")
+        try:
+            C.compile_asm(asm)
+        except (OSError, subprocess.CalledProcessError) as e:
+            pytest.skip("hipcc unavailable: %s" % e)
+        res = C.check(asm)
+    waits = {(k, n) for k, n, _ in res}
+    assert {n for _, n in waits} == {2, 3}, res           # both the spatial and the temporal wait
+    assert len({k for k, _ in waits}) == 3, res           # in each family's kernel
+    assert all(ops >= n for _, n, ops in res), res
