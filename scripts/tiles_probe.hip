@@ -131,6 +131,34 @@ int main(int argc, char** argv)
     SHAPE(2, 4, 1, 3)
 #undef SHAPE
     run("tilesP4_video", c3v, 0, 4, [](const FrameSet& p) { return launch_vec<0, 4>(p, 0); });
+    // angle P4 schedules: the product shape with the
+    // row pieces cut shorter (more items than resident slots, frame-major
+    // order, consecutive pieces of a frame on one XCD or spread), as the
+    // predictor (K = 4) and as a copy through the same ring (K = 0)
+    auto sched = [](const FrameSet& p, int K, int rows, int xcd) -> hipError_t {
+        const void* fn = K ? (const void*)predict_vec<1, 4, 15, 1, 4, 1, 3> : (const void*)predict_vec<1, 0, 15, 1, 4, 1, 3>;
+        Plan pl;
+        hipError_t e = make_plan_shape(p, fn, 4 * 64 + 64, 4, 3, 512, kVHalo, 1, pl);
+        if (e != hipSuccess) return e;
+        if (rows > 0) {
+            pl.rows_per_piece = rows;
+            pl.npiece = (p.H + rows - 1) / rows;
+            pl.grid = p.nz * pl.npiece * pl.nstrip;
+        }
+        if (xcd >= 0) pl.xcd_map = xcd && (p.nz * pl.npiece) % 8 == 0 && pl.nstrip > 1;
+        return launch_plan(fn, p, pl, 4, 1, 0);
+    };
+#define SCHED(K, ROWS, XCD)                                                                                  \
+    run("angle_sched_k" #K "_rows" #ROWS "_xcd" #XCD, c3, 1, K,                                            \
+        [&](const FrameSet& p) { return sched(p, K, ROWS, XCD); });
+    SCHED(4, 0, -1) SCHED(0, 0, -1)
+    SCHED(4, 0, 0) SCHED(0, 0, 0)
+    SCHED(4, 256, 1) SCHED(0, 256, 1)
+    SCHED(4, 128, 1) SCHED(0, 128, 1)
+    SCHED(4, 64, 1) SCHED(0, 64, 1)
+    SCHED(4, 2048, 1) SCHED(0, 2048, 1)
+    SCHED(4, 128, 0) SCHED(0, 128, 0)
+#undef SCHED
     run("tilesP4_c5", c5, 0, 4, [](const FrameSet& p) { return launch_vec<0, 4>(p, 0); });
     using S0v = VecShape<0>;
     run("tilesP4_c5_single", c5, 0, 4,  // round-3 path: temporal frames re-read frame z - 1 (P ring)
