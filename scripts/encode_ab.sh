@@ -2,7 +2,7 @@
 # Encode A/B on one box: the bench's timed leg only (config 3, N = 1) under
 # several environment settings, each run twice, interleaved.
 # usage: scripts/encode_ab.sh OUTFILE "ENV1" "ENV2" ...   ("" = defaults)
-set -u
+set -u -o pipefail
 OUT=$1; shift
 : > "$OUT"
 for rep in 1 2; do

@@ -2,7 +2,7 @@
 # PMC passes over one probe of a stand-alone probe binary (counters only with
 # --kernel-trace; each pass its own run under a hard time limit).
 # usage: scripts/pmc_probe.sh OUTDIR KERNEL_REGEX -- <probe command...>
-set -u
+set -u -o pipefail
 OUT=$1; shift
 RX=$1; shift; shift
 mkdir -p "$OUT"
