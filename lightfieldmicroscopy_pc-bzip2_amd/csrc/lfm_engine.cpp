@@ -1149,11 +1149,37 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     // pipelined encodes: the next submit starts once every batch of the last
     // round has passed the release stage (hook of lfm_hip_bzip2_blocks)
     const int release_at = pipe_release_stage();
+    // LFM_BZ2_STAGGER=1 / 2 (experiment): slot 1 starts its first batch once
+    // slot 0's first batch has passed its BWT / MTF stage, so the slots'
+    // latency-bound stages (MTF, Huffman tables) run beside the other slot's
+    // sorts instead of in lockstep
+    static const int stagger = [] {
+        const char* e = std::getenv("LFM_BZ2_STAGGER");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 1 || v == 2 ? v : 0;
+    }();
     struct HookCtx {
         Inflight* fly;
-        int stage;
+        int stage;       // release stage for the pipelined encodes (fly)
+        int stagger;     // stage that lets slot 1 start (0: none)
+        std::mutex* mu;
+        std::condition_variable* cv;
+        bool* go;        // slot 1 may start
     };
-    HookCtx hctx{fly, release_at};
+    bool stagger_go = !stagger || nslots < 2;
+    HookCtx hctx{fly, release_at, 0, &mu, &cv, &stagger_go};
+    HookCtx sctx{fly, release_at, stagger, &mu, &cv, &stagger_go};
+    auto hook = [](void* ctx, int stage) {
+        HookCtx* c = (HookCtx*)ctx;
+        if (c->fly && c->stage > 0 && stage == c->stage) c->fly->reach();
+        if (c->stagger && stage == c->stagger) {
+            {
+                std::lock_guard<std::mutex> lk(*c->mu);
+                *c->go = true;
+            }
+            c->cv->notify_all();
+        }
+    };
     // host stack still uploading (start_upload): a batch waits for the chunks
     // holding its last block (blocks run x -> y -> z -> c -> t, so that block
     // reaches furthest into the flattened (t, c, z) frame order)
@@ -1171,13 +1197,13 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         (void)hipSetDevice(device_);
         BzSlot& sl = bz_[k];
         for (uint64_t b = k; b < nbatch; b += nslots) {
-            if (fly && release_at > 0 && b + nslots >= nbatch)
-                lfm_hip_bzip2_set_stage_hook(
-                    [](void* ctx, int stage) {
-                        HookCtx* c = (HookCtx*)ctx;
-                        if (stage == c->stage) c->fly->reach();
-                    },
-                    &hctx);
+            const bool rel_hook = fly && release_at > 0 && b + nslots >= nbatch;
+            const bool stg_hook = !stagger_go && b == 0;  // slot 0's first batch lets slot 1 go
+            if (rel_hook || stg_hook) lfm_hip_bzip2_set_stage_hook(hook, stg_hook ? (void*)&sctx : (void*)&hctx);
+            if (k == 1 && b == 1) {  // slot 1's first batch waits for the stagger point
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stagger_go || abort_all.load(); });
+            }
             if (b >= (uint64_t)nslots) {  // wait until the writer consumed batch b - nslots
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return state[b - nslots] != 1 || abort_all.load(); });
@@ -1195,9 +1221,14 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             }
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
                                           ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
-            if (fly && b + nslots >= nbatch) {
-                if (release_at == 0) fly->reach();
-                lfm_hip_bzip2_set_stage_hook(nullptr, nullptr);
+            if (fly && b + nslots >= nbatch && release_at == 0) fly->reach();
+            if (rel_hook || stg_hook) lfm_hip_bzip2_set_stage_hook(nullptr, nullptr);
+            if (stg_hook) {  // (also when the batch never reached the stage)
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    stagger_go = true;
+                }
+                cv.notify_all();
             }
             float sm[5];
             if (ok && lfm_hip_bzip2_last_stage_ms(sm) == 0)
