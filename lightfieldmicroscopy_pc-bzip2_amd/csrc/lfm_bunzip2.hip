@@ -260,6 +260,17 @@ struct LaneBits {
             win = (win << 32) | next();
         }
     }
+    // skip with the refill test on a scalar copy of off (equal in every
+    // lane): a uniform s_cbranch instead of an exec-mask branch (save / test
+    // / restore exec on the CU's one scalar unit, per symbol)
+    __device__ __forceinline__ void skip_u(uint32_t nb)
+    {
+        off += nb;
+        if ((uint32_t)__builtin_amdgcn_readfirstlane((int)off) >= 32u) {
+            off -= 32;
+            win = (win << 32) | next();
+        }
+    }
     __device__ __forceinline__ bool over() const { return 32 * (wi - 2) + off > total; }
 };
 
@@ -462,7 +473,8 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                 const uint32_t e = lut[tb + lb.peek(LB)];
                 uint32_t len = e >> 9;
                 uint32_t sym = e & 511u;
-                if (len == 0) {
+                // a code longer than LB bits: a uniform (scalar) branch, see skip_u
+                if (__builtin_amdgcn_readfirstlane((int)len) == 0) {
                     const uint32_t t = tb >> LB;
                     uint32_t zn = LB + 1;
                     int32_t zvec = (int32_t)lb.peek(zn);
@@ -480,17 +492,24 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
                     }
                     len = zn;
                 }
-                lb.skip(len);
+                lb.skip_u(len);
                 return sym;
             };
             uint32_t symv = 0, G = 0;
             if (g < nSel) {  // not the last group: 50 symbols, none of them EOB (libbzip2 writes
                              // one selector per group, EOB in the last; anything else -> host)
                 if constexpr (VB) {
-                    for (G = 0; G < 50; ++G) {
-                        const uint32_t sym = decode1v();
-                        symv = lane == G ? sym : symv;
+                    // 5 x 10 symbols: the lane compare against a constant, loop
+                    // control once per 10 symbols
+                    for (uint32_t G0 = 0; G0 < 50; G0 += 10) {
+                        const uint32_t dl = lane - G0;
+#pragma unroll
+                        for (uint32_t u = 0; u < 10; ++u) {
+                            const uint32_t sym = decode1v();
+                            symv = dl == u ? sym : symv;
+                        }
                     }
+                    G = 50;
                 } else {
                     for (G = 0; G < 50; ++G) put(symv, decode1(), G);
                 }
