@@ -628,6 +628,72 @@ def test_pipelined_submit_wait(lfmlib, oracle, gpu):
         lfmlib.set_family("tiles")
 
 
+_UPLOAD_CHILD = r"""
+import json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import torch, lfm, lfm_oracle as O
+torch.cuda.set_device(0)
+out = {}
+enc = lfm.Encoder(device=0)
+# 1. tiles video stack: 1-MiB chunks (4 frames of 512 x 256), a 2-MiB ring
+#    (2 slots: every slot reused, temporal predecessors across chunk edges)
+img = O.synthetic_lf(512, 256, Z=21, T=13, seed=41)
+lfm.set_family("tiles")
+out["video"] = enc.encode(img, header_version=0x80, nnum=13)[0] == O.encode(img, header_version=0x80, nnum=13,
+                                                                               family="tiles")
+# 2. 5-D stack (c = 2, t = 3): chunks never cross a (c, t) volume
+img5 = O.synthetic_lf(520, 200, Z=5, C=2, Tn=3, T=15, seed=42)
+out["5d"] = enc.encode(img5, header_version=8 + 5, nnum=15, block_size=[64, 64, 2, 1, 1])[0] == O.encode(
+    img5, header_version=8 + 5, nnum=15, family="tiles", block_size=[64, 64, 2, 1, 1])
+# 3. a z-slab of a video stack starting at an odd frame, host input: its
+#    previous raw frame comes from the host
+full = O.synthetic_lf(512, 256, Z=17, T=13, seed=43)[0, 0]
+k, _ = lfm.select_device(torch.from_numpy(full[0].view(np.int16)).cuda(), 512, 256, 13, "tiles")
+bs = [64, 64, 3, 1, 1]
+a, _ = enc.encode_slab(full[:9], 0, header_version=0x80 | (8 + k), nnum=13, block_size=bs)
+b, _ = enc.encode_slab(full[9:], 9, prev=full[8], header_version=0x80 | (8 + k), nnum=13, block_size=bs)
+out["slab"] = lfm.merge_slabs([a, b]) == O.encode(full, header_version=0x80, nnum=13, family="tiles",
+                                                  block_size=bs)
+# 4. pipelined host submits: after submit returns the stack may be refilled
+stacks = [O.synthetic_lf(512, 256, Z=16, T=15, seed=50 + i)[0, 0] for i in range(3)]
+lfm.set_family("angle")
+exp = [O.encode(s.copy(), header_version=0, nnum=15, family="angle") for s in stacks]
+buf = np.empty_like(stacks[0])
+got, prev = [], None
+for s in stacks:
+    buf[...] = s
+    t = enc.submit(buf, header_version=0, nnum=15)
+    buf[...] = 0x1234  # the upload is complete when submit returns
+    if prev is not None:
+        got.append(enc.wait(prev)[0])
+    prev = t
+got.append(enc.wait(prev)[0])
+out["pipelined"] = got == exp
+enc.close()
+print(json.dumps(out))
+"""
+
+
+def test_host_upload_pipe_chunks_and_ring(gpu, tmp_path):
+    """Host stacks upload in chunks through a ring of device slots, each chunk
+    predicted as it lands and every GPU-bzip2 batch waiting only for its
+    chunks (UploadPipe).  With 1-MiB chunks and a 2-slot ring every slot is
+    reused: video stacks (temporal predecessors across chunk edges), 5-D
+    stacks, an odd-start video slab with its previous frame from the host, and
+    pipelined host submits (the stack refilled as soon as submit returns)
+    give the oracle's bytes."""
+    import subprocess
+    import sys
+    from conftest import PKG, REPO
+    env = dict(os.environ, LFM_H2D_CHUNK_MB="1", LFM_H2D_RING_MB="2")
+    r = subprocess.run([sys.executable, "-c", _UPLOAD_CHILD, PKG, os.path.join(REPO, "oracle")], env=env,
+                       capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got == {"video": True, "5d": True, "slab": True, "pipelined": True}, got
+
+
 def test_submit_releases_unpredicted_device_input(lfmlib, oracle, gpu):
     """A submit whose stack skips the predictor stage (forced predictor 0,
     request 8) returns with the caller's device image no longer referenced:
