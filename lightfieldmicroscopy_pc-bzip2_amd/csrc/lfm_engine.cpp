@@ -2154,20 +2154,24 @@ int decode_roi(const uint8_t* payload, size_t len, const klb_image_header& h, co
         const uint64_t id = ids[i], sz = h.getBlockCompressedSizeBytes(id);
         std::memcpy(spay.data() + (sub.blockOffset[i] - sz), payload + h.getBlockOffset(id), sz);
     });
+    // a region that is exactly its blocks' box (e.g. whole t-volumes) is
+    // decoded straight into `out`: no temporary image, no crop
+    bool exact = true;
+    for (int d = 0; d < 5; ++d) exact = exact && o[d] == lb[d] && n[d] == (uint64_t)ub[d] - lb[d] + 1;
+    if (exact) return decode_payload(spay.data(), spay.size(), sub, out, threads, family);
     std::unique_ptr<uint8_t[]> simg(new uint8_t[sub.getImageSizeBytes()]);  // (no zero fill: every byte is decoded)
     const int rc = decode_payload(spay.data(), spay.size(), sub, simg.get(), threads, family);
     if (rc) return rc;
     const size_t row = (size_t)(ub[0] - lb[0] + 1) * bpp;
-    uint8_t* q = out;
-    for (uint64_t t = lb[4]; t <= ub[4]; ++t)
-        for (uint64_t c = lb[3]; c <= ub[3]; ++c)
-            for (uint64_t z = lb[2]; z <= ub[2]; ++z)
-                for (uint64_t y = lb[1]; y <= ub[1]; ++y) {
-                    const uint64_t e = (lb[0] - o[0]) +
-                                       n[0] * ((y - o[1]) + n[1] * ((z - o[2]) + n[2] * ((c - o[3]) + n[3] * (t - o[4]))));
-                    std::memcpy(q, simg.get() + e * bpp, row);
-                    q += row;
-                }
+    const uint64_t ny = (uint64_t)ub[1] - lb[1] + 1, nz = (uint64_t)ub[2] - lb[2] + 1, nc = (uint64_t)ub[3] - lb[3] + 1;
+    const uint64_t nrows = ny * nz * nc * ((uint64_t)ub[4] - lb[4] + 1);
+    parallel_for(nrows, threads, [&](uint64_t r) {  // output row r = ((t * nc + c) * nz + z) * ny + y
+        const uint64_t y = lb[1] + r % ny, z = lb[2] + (r / ny) % nz, c = lb[3] + (r / ny / nz) % nc,
+                       t = lb[4] + r / ny / nz / nc;
+        const uint64_t e = (lb[0] - o[0]) +
+                           n[0] * ((y - o[1]) + n[1] * ((z - o[2]) + n[2] * ((c - o[3]) + n[3] * (t - o[4]))));
+        std::memcpy(out + r * row, simg.get() + e * bpp, row);
+    });
     return 0;
 }
 

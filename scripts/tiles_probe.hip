@@ -115,7 +115,7 @@ int main(int argc, char** argv)
         const double alg6 = alg + (s.video ? 2.0 * (double)s.W * s.H * (s.Z / 2) : 0.0);
         printf("{\"probe\": \"%s\", \"shape\": [%d, %d, %d, %d, %d], \"ms\": %.4f, \"frac_8TBs\": %.4f, "
                "\"frac_8TBs_per_frame_bytes\": %.4f, \"mismatch\": %lld}\n",
-               name, s.W, s.H, s.Z, s.T, s.video, ms, alg / ms / 1e9 / 8000.0, alg6 / ms / 1e9 / 8000.0, mism);
+               name, s.W, s.H, s.Z, s.T, s.video, ms, alg / ms / 1e6 / 8000.0, alg6 / ms / 1e6 / 8000.0, mism);
         fflush(stdout);
     };
     auto run = [&](const char* name, Shape s, int fam, int k, auto launch) { run_prep(name, s, fam, k, launch, ident); };
