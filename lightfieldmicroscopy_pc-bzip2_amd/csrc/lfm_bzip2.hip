@@ -123,7 +123,6 @@ struct Batch {
     uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
     uint32_t* wide_cnt;
     uint32_t tie_direct;     // tie_runs_direct resolves short runs of equal prefixes from the text (LFM_TIE_DIRECT)
-    uint32_t heap_lookahead; // Huffman heap sifts read two levels ahead (LFM_HEAP_LOOKAHEAD, default 1)
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -2540,41 +2539,7 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
         // either next node), then the level is decided from the children in
         // registers; ea = address of the entry the key may land in, ca = the
         // children pair of zz (ea of the next level is ca + 4 * right)
-        // Two levels ahead (LFM_HEAP_LOOKAHEAD, default): a level also holds
-        // its grandchildren quad in registers and reads the two quads of its
-        // great-grandchildren, which the NEXT level selects from -- every LDS
-        // read has a whole level of compares to land in, not part of one.
-        auto quad = [&](uint32_t q) -> HeapQuad<Ent> {
-            return *(const HeapQuad<Ent>*)(hb + min(q, (uint32_t)kQuads - 1u) * QS + lb);
-        };
-        auto sift2 = [&](int nHeap, Ent k) {
-            uint32_t zz = 1, ea = lb + ES, ca = lb + 2u * ES;
-            Ent cx = ent(2), cy = ent(3), root = k;
-            HeapQuad<Ent> g = quad(1);  // grandchildren of the root: entries 4 .. 7
-            bool go = true, first = true;
-            while (true) {
-                const HeapQuad<Ent> h0 = quad(2u * zz), h1 = quad(2u * zz + 1u);
-                __builtin_amdgcn_sched_barrier(0);  // the reads go out before the level's compares
-                const uint32_t ga = min(zz, (uint32_t)kQuads - 1u) * QS + lb;
-                const uint32_t yy = zz << 1;
-                const bool r = yy < (uint32_t)nHeap && cy < (cx & kW);
-                const Ent ky = r ? cy : cx;
-                go = go && yy <= (uint32_t)nHeap && !(k < (ky & kW));
-                *(Ent*)(hb + ea) = ky;  // a stopped lane's stray write is overwritten below
-                if (first) root = go ? ky : k;
-                first = false;
-                ea = go ? ca + (r ? ES : 0u) : ea;
-                ca = ga + (r ? 2u * ES : 0u);
-                zz = go ? yy + (r ? 1u : 0u) : zz;
-                cx = r ? g.e[2] : g.e[0];
-                cy = r ? g.e[3] : g.e[1];
-                g = r ? h1 : h0;  // grandchildren of the next node (quad 2 zz + r)
-                if (!__any(go)) break;
-            }
-            *(Ent*)(hb + ea) = k;
-            return root;
-        };
-        auto sift1 = [&](int nHeap, Ent k) {
+        auto sift = [&](int nHeap, Ent k) {
             uint32_t zz = 1, ea = lb + ES, ca = lb + 2u * ES;
             Ent cx = ent(2), cy = ent(3), root = k;
             bool go = true, first = true;
@@ -2599,7 +2564,6 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             *(Ent*)(hb + ea) = k;
             return root;
         };
-        auto sift = [&](int nHeap, Ent k) { return B.heap_lookahead ? sift2(nHeap, k) : sift1(nHeap, k); };
         auto upheap = [&](uint32_t z, Ent k) {  // returns the final position
             bool go = true;
             while (true) {
@@ -3344,11 +3308,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.nblock_max = 100000u * level - 19u;
     static const uint32_t tie_direct = !(std::getenv("LFM_TIE_DIRECT") && std::atoi(std::getenv("LFM_TIE_DIRECT")) == 0);
     B.tie_direct = tie_direct;
-    static const uint32_t heap_lookahead = [] {
-        const char* e = std::getenv("LFM_HEAP_LOOKAHEAD");
-        return (uint32_t)!(e && std::atoi(e) == 0);
-    }();
-    B.heap_lookahead = heap_lookahead;
     if (ws_bytes < lfm_hip_bzip2_workspace_bytes(count, raw_cap)) return LFM_HIP_EINVAL;
     const size_t N = (size_t)count * B.cap;
     if (N >= (1ull << 32)) return LFM_HIP_EINVAL;
