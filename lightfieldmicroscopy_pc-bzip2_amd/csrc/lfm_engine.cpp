@@ -446,8 +446,10 @@ Encoder::~Encoder()
     join_inflight();
     for (UploadPipe& u : up_) u.join();
     if (gpu_ready_) {
-        for (UploadPipe& u : up_)
+        for (UploadPipe& u : up_) {
             for (hipEvent_t e : u.ev) (void)hipEventDestroy(e);
+            u.release_sdma();
+        }
         if (up_stream_) (void)hipStreamDestroy(up_stream_);
         (void)hipSetDevice(device_);
         if (d_in_) (void)hipFree(d_in_);
@@ -713,6 +715,17 @@ int Encoder::UploadPipe::wait_frames(uint64_t f_end, hipStream_t st)
     return hipStreamWaitEvent(st, ev[3 * c + 2], 0) == hipSuccess ? 0 : 3;
 }
 
+void Encoder::UploadPipe::release_sdma()
+{
+    for (int i = 0; i < 2; ++i) {
+        if (sig[i]) hsa_signal_destroy(hsa_signal_t{sig[i]});
+        if (stage[i]) (void)hipHostFree(stage[i]);
+        sig[i] = 0;
+        stage[i] = nullptr;
+    }
+    stage_cap = 0;
+}
+
 void Encoder::UploadPipe::join()
 {
     if (th.joinable()) th.join();
@@ -792,11 +805,114 @@ int Encoder::start_upload(const void* img, klb_image_header& h, const SlabSpec& 
     uint16_t* const d_in = (uint16_t*)d_in_;
     uint16_t* const d_sym = (uint16_t*)d_sym_[set];
     const uint8_t* const src = (const uint8_t*)img;
+    // copies on an SDMA engine (LFM_H2D_SDMA=0: hipMemcpyAsync, whose blit
+    // kernel measured ~25 ms slower for the GPU bzip2 running beside a 2 GiB
+    // upload); a pinned (HSA-allocated) source goes straight to the engine,
+    // a pageable one through two pinned staging chunks (host copy of one
+    // overlapping the engine's copy of the other)
+    static const bool sdma_on = env_int("LFM_H2D_SDMA", 1) != 0;
+    const hsa_agent_t* cpu = sdma_on ? hsa_cpu_agent() : nullptr;
+    hsa_agent_t gpu{};
+    bool direct = false;
+    if (cpu) {
+        hsa_amd_pointer_info_t info;
+        std::memset(&info, 0, sizeof(info));
+        info.size = sizeof(info);
+        if (hsa_amd_pointer_info(d_in_, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+            info.type != HSA_EXT_POINTER_TYPE_HSA)
+            cpu = nullptr;
+        else
+            gpu = info.agentOwner;
+    }
+    if (cpu) {
+        hsa_amd_pointer_info_t info;
+        std::memset(&info, 0, sizeof(info));
+        info.size = sizeof(info);
+        direct = hsa_amd_pointer_info((void*)img, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS &&
+                 info.type == HSA_EXT_POINTER_TYPE_HSA;
+        for (int i = 0; i < 2 && cpu; ++i) {
+            hsa_signal_t sg;
+            if (!up.sig[i]) {
+                if (hsa_signal_create(0, 0, nullptr, &sg) != HSA_STATUS_SUCCESS) cpu = nullptr;
+                else up.sig[i] = sg.handle;
+            }
+        }
+        if (cpu && !direct && up.stage_cap < cbytes) {
+            for (int i = 0; i < 2; ++i) {
+                if (up.stage[i]) (void)hipHostFree(up.stage[i]);
+                up.stage[i] = nullptr;
+            }
+            up.stage_cap = 0;
+            if (hipHostMalloc(&up.stage[0], cbytes, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(&up.stage[1], cbytes, hipHostMallocDefault) != hipSuccess)
+                cpu = nullptr;
+            else
+                up.stage_cap = cbytes;
+        }
+    }
+    const int cthreads = default_threads();
     up.th = std::thread([=, &up]() {
         (void)hipSetDevice(device_);
         auto t0 = clk::now();
         int rc = 0;
-        for (uint64_t c = 0; c < nch && !rc; ++c) {
+        auto predict = [&](uint64_t c, uint16_t* slot) -> int {
+            const uint64_t v = c / per_vol, za = (c % per_vol) * cz, zb = std::min<uint64_t>(Z, za + cz);
+            hipEvent_t* e = &up.ev[3 * c];
+            const uint16_t* prev = nullptr;
+            if (video) prev = za > 0 ? d_in + ((c - 1) % nslot) * cz * fpx + (cz - 1) * fpx : d_prev;
+            (void)hipEventRecord(e[1], stream_);
+            if (lfm_hip_predict(slot, prev, d_sym + (v * Z + za) * fpx, (int)W, (int)H, (int)(zb - za), T, fam, k,
+                                video, (int)(z0 + za), stream_) != LFM_HIP_OK ||
+                hipEventRecord(e[2], stream_) != hipSuccess)
+                return 3;
+            {
+                std::lock_guard<std::mutex> lk(up.mu);
+                up.recorded = c + 1;
+            }
+            up.cv.notify_all();
+            return 0;
+        };
+        auto sig_wait = [&](int b) {
+            return hsa_signal_wait_scacquire(hsa_signal_t{up.sig[b]}, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
+                                             HSA_WAIT_STATE_BLOCKED) == 0;
+        };
+        // SDMA: copy c is issued before chunk c - 1 (copied) is predicted,
+        // so the engine always has the next chunk while a chunk is predicted
+        for (uint64_t c = 0; cpu && c < nch && !rc; ++c) {
+            const uint64_t v = c / per_vol, za = (c % per_vol) * cz, zb = std::min<uint64_t>(Z, za + cz);
+            const size_t len = (zb - za) * fs;
+            const int b = (int)(c & 1);
+            uint16_t* slot = d_in + (c % nslot) * cz * fpx;
+            // the slot's last readers (chunk c - nslot and the chunk after
+            // it, which reads its last frame) are predicted
+            if (c >= nslot && hipEventSynchronize(up.ev[3 * (c - nslot + 1) + 2]) != hipSuccess) rc = 3;
+            if (!rc && c >= 2 && !sig_wait(b)) rc = 3;  // (chunk c - 2's copy: staging chunk b is free)
+            const uint8_t* from = src + (v * Z + za) * fs;
+            if (!rc && !direct) {
+                par_memcpy(up.stage[b], from, len, cthreads);
+                from = (const uint8_t*)up.stage[b];
+            }
+            if (!rc) {
+                hsa_signal_store_relaxed(hsa_signal_t{up.sig[b]}, 1);
+                if (hsa_amd_memory_async_copy(slot, gpu, from, *cpu, len, 0, nullptr, hsa_signal_t{up.sig[b]}) !=
+                    HSA_STATUS_SUCCESS) {
+                    hsa_signal_store_relaxed(hsa_signal_t{up.sig[b]}, 0);
+                    rc = 3;
+                }
+            }
+            if (!rc && c >= 1) {
+                if (!sig_wait((int)((c - 1) & 1))) rc = 3;
+                else rc = predict(c - 1, d_in + ((c - 1) % nslot) * cz * fpx);
+            }
+        }
+        if (cpu && !rc) {
+            if (!sig_wait((int)((nch - 1) & 1))) rc = 3;
+            else rc = predict(nch - 1, d_in + ((nch - 1) % nslot) * cz * fpx);
+        }
+        if (cpu) {  // no copy still reads the caller's image or a staging chunk
+            for (int b = 0; b < 2; ++b) (void)sig_wait(b);
+        }
+        for (uint64_t c = 0; !cpu && c < nch && !rc; ++c) {
             const uint64_t v = c / per_vol, za = (c % per_vol) * cz, zb = std::min<uint64_t>(Z, za + cz);
             uint16_t* slot = d_in + (c % nslot) * cz * fpx;
             hipEvent_t* e = &up.ev[3 * c];

@@ -187,6 +187,13 @@ private:
         int rc = 0;
         bool active = false;
         double h2d_ms = 0.0, predict_ms = 0.0;
+        // SDMA copies (HSA async copies, not a blit kernel beside the GPU
+        // bzip2): completion signals and, for pageable sources, two pinned
+        // staging chunks; kept between encodes
+        uint64_t sig[2] = {0, 0};
+        void* stage[2] = {nullptr, nullptr};
+        size_t stage_cap = 0;
+        void release_sdma();
         // make `st` wait until frames [0, f_end) are predicted (0 or 3)
         int wait_frames(uint64_t f_end, hipStream_t st);
         void join();
