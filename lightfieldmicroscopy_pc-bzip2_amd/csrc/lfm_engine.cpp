@@ -686,6 +686,14 @@ int Encoder::ensure_gpu()
         hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
     }
+    // the first buffer set's GPU bzip2 slot streams are created right after
+    // the predictor stream, so each lands on a hardware queue of its own
+    // (GPU_MAX_HW_QUEUES is 4, the null stream holding one): streams created
+    // later share queues, and two slots sharing one run their batches in
+    // series (measured: the upload pipe's extra stream, created first, put
+    // both slots on one queue, +19 ms per 2 GiB encode)
+    for (int k = 0; k < bz_slot_count(); ++k)
+        if (hipStreamCreateWithFlags(&bz_[0][k].stream, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
     (void)hipEventCreate(&ev0_);
     (void)hipEventCreate(&ev1_);
     gpu_ready_ = true;
@@ -733,6 +741,15 @@ void Encoder::UploadPipe::join()
     active = false;
 }
 
+int Encoder::bz_slot_count()
+{
+    static const int n = [] {
+        const int v = env_int("LFM_BZ2_SLOTS", 0);
+        return v > 0 ? std::min(v, (int)kBzSlots) : 2;
+    }();
+    return n;
+}
+
 bool Encoder::upload_pipe_ok(bool dev, const klb_image_header& h) const
 {
     static const bool on = [] {
@@ -777,7 +794,6 @@ int Encoder::start_upload(const void* img, klb_image_header& h, const SlabSpec& 
     const uint64_t nslot = std::min<uint64_t>(nch, std::max<uint64_t>(2, ring_target / cbytes));
     if (!dev_alloc(d_in_, d_in_cap_, nslot * cbytes)) return 3;
     if (!dev_alloc(d_sym_[set], d_sym_cap_[set], V * Z * fs)) return 3;
-    if (!up_stream_ && hipStreamCreateWithFlags(&up_stream_, hipStreamNonBlocking) != hipSuccess) return 3;
     while (up.ev.size() < 3 * nch) {
         hipEvent_t e = nullptr;
         if (hipEventCreate(&e) != hipSuccess) return 3;
@@ -850,6 +866,8 @@ int Encoder::start_upload(const void* img, klb_image_header& h, const SlabSpec& 
                 up.stage_cap = cbytes;
         }
     }
+    // (the stream of the hipMemcpyAsync copies only: SDMA copies need none)
+    if (!cpu && !up_stream_ && hipStreamCreateWithFlags(&up_stream_, hipStreamNonBlocking) != hipSuccess) return 3;
     const int cthreads = default_threads();
     up.th = std::thread([=, &up]() {
         (void)hipSetDevice(device_);
@@ -942,7 +960,7 @@ int Encoder::start_upload(const void* img, klb_image_header& h, const SlabSpec& 
             up.cv.notify_all();
         }
         // the host image is no longer read once the copies are done
-        if (hipStreamSynchronize(up_stream_) != hipSuccess) rc = 3;
+        if (!cpu && hipStreamSynchronize(up_stream_) != hipSuccess) rc = 3;
         const double h2d = ms_since(t0);
         double pms = 0.0;
         if (!rc && hipEventSynchronize(up.ev[3 * (nch - 1) + 2]) == hipSuccess) {
@@ -1217,11 +1235,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         const long v = e ? std::atol(e) : 0;
         return (uint64_t)(v > 0 ? v : 1);
     }();
-    static const int slots = [] {
-        const char* e = std::getenv("LFM_BZ2_SLOTS");
-        const int v = e ? std::atoi(e) : 0;
-        return v > 0 ? std::min(v, (int)kBzSlots) : 2;
-    }();
+    const int slots = bz_slot_count();
     const uint64_t nway = slots * per_slot;
     uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>((nblocks + nway - 1) / nway,
                                                                 budget / slots / per_stream));

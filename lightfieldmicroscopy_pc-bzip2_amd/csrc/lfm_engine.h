@@ -235,6 +235,7 @@ private:
         void* h_out = nullptr; size_t h_out_cap = 0;
     };
     BzSlot bz_[2][kBzSlots];
+    static int bz_slot_count();  // slots that run (env LFM_BZ2_SLOTS, default 2)
     void* h_sym_[2] = {nullptr, nullptr}; size_t h_sym_cap_[2] = {0, 0};   // pinned, by buffer set
 };
 
