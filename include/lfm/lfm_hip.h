@@ -104,6 +104,14 @@ size_t lfm_hip_bunzip2_workspace_bytes(uint32_t count, uint32_t out_stride);
 int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_offs, uint32_t count, void* d_out,
                            uint32_t out_stride, void* d_ws, size_t ws_bytes, uint32_t* h_lens, uint32_t* h_flags,
                            void* stream);
+/* lfm_hip_bunzip2_blocks without the final synchronisation: returns once the
+ * kernels and the copies into h_lens / h_flags are queued on `stream`
+ * (h_lens / h_flags must be pinned host memory; read them after the stream or
+ * an event recorded behind the call has completed).  The pipelined decode
+ * (gpu_decode) overlaps one chunk's kernels with another's copies. */
+int lfm_hip_bunzip2_issue(const void* d_payload, const uint64_t* h_offs, uint32_t count, void* d_out,
+                          uint32_t out_stride, void* d_ws, size_t ws_bytes, uint32_t* h_lens, uint32_t* h_flags,
+                          void* stream);
 
 /* Decoded blocks first .. first + count - 1 (block i at d_blocks + (i -
  * first) * stride, x fastest) back into the device image (the inverse of the

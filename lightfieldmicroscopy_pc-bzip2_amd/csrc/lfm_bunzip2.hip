@@ -36,6 +36,10 @@
 #include <vector>
 #include "lfm_hip.h"
 
+#ifndef LFM_BZD_PROBE
+#define LFM_BZD_PROBE 0  // timing probes of bzd_huff (scripts only; 0 in the library)
+#endif
+
 namespace lfm {
 namespace bzd {
 
@@ -530,6 +534,10 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             }
             if (VB && __ballot(vbad)) flag = kHost;
             if (flag) break;
+#if LFM_BZD_PROBE >= 3  // timing probe (wrong output): the symbol decode alone
+            nblock = min(nblock + G, D.cap - 64);
+            continue;
+#endif
             // 2. runs and counts over the lanes
             const bool valid = lane < G;
             const bool isrun = valid && symv <= 1u;
@@ -542,22 +550,41 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             // the move-to-front chain over the group's ordinary symbols
             const uint32_t front0 = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, 0) & 0xFFu;
             uint32_t outb = 0;
+            // per-lane operands of the steps, worked out for all lanes at once
+            // (each step reads its three by readlane): the list word and byte
+            // shift of position nn = sym - 1, and 8 * nn for the entry mask
+            const uint32_t nnv = symv - 1u;
+            const uint32_t wiv = (nnv >> 2) & 63u, shv = 8u * (nnv & 3u), nn8v = 8u * nnv;
+            const int kk08 = 8 * kk0;
+#if LFM_BZD_PROBE >= 1  // timing probe (wrong output): no move-to-front chain
+            outb = symv;
+            for (uint64_t nm = 0; nm;) {
+#else
             for (uint64_t nm = __ballot(isnorm); nm;) {
+#endif
                 const uint32_t k = (uint32_t)__builtin_ctzll(nm);
-                nm &= ~(1ull << k);
-                const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)symv, (int)k) - 1u;
-                const uint32_t v =
-                    ((uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)((nn >> 2) & 63u)) >> (8 * (nn & 3))) & 0xFFu;
+                asm("s_bitset0_b64 %0, %1" : "+s"(nm) : "s"(k));  // (one SALU op, not shift + and-not)
+                const uint32_t wi = (uint32_t)__builtin_amdgcn_readlane((int)wiv, (int)k);
+                const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)shv, (int)k);
+                const int nn8 = __builtin_amdgcn_readlane((int)nn8v, (int)k);
+                // v = list[nn] (the low byte of vw; the output keeps only that byte)
+                const uint32_t vw = (uint32_t)__builtin_amdgcn_readlane((int)mtfw, (int)wi) >> sh;
+                uint32_t v24;  // vw << 24 straight into a VGPR (the DPP's lane-0 value)
+                asm("v_lshlrev_b32_e64 %0, 24, %1" : "=v"(v24) : "s"(vw));
                 // move to front: entries 0 .. nn shift up by one, v goes to 0
                 // lane l - 1's word (DPP wave_shr:1, a VALU op); lane 0 gets v << 24
-                const uint32_t up =
-                    (uint32_t)__builtin_amdgcn_update_dpp((int)(v << 24), (int)mtfw, 0x138, 0xF, 0xF, false);
-                const uint32_t sh = (mtfw << 8) | (up >> 24);
-                const int kq = min(4, max(0, (int)nn + kk0));  // entries of this lane at <= nn
-                const uint32_t msk = kq >= 4 ? 0xFFFFFFFFu : ((1u << (8 * kq)) - 1u);
-                mtfw = (sh & msk) | (mtfw & ~msk);
-                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(outb) : "s"(v), "s"(k) : "m0");
+                const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)v24, (int)mtfw, 0x138, 0xF, 0xF, false);
+                const uint32_t shf = __builtin_amdgcn_alignbit(mtfw, up, 24);  // (mtfw << 8) | (up >> 24)
+                // this lane's entries above nn keep their place: the bytes from
+                // 8 * clamp(nn + 1 - 4 * lane, 0, 4) up (all of them: 0, none: 32)
+                const int t8 = min(32, max(0, nn8 + kk08));
+                const uint32_t keep = (uint32_t)(~0ull << t8);
+                mtfw = (mtfw & keep) | (shf & ~keep);
+                // (lane select in m0: an SGPR source and an SGPR lane select
+                // together exceed gfx9's one constant-bus read)
+                asm("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(outb) : "s"(vw), "s"(k) : "m0");
             }
+            outb &= 0xFFu;
             // a run repeats the list front: the byte of the last ordinary symbol before it
             const uint32_t fb = (uint32_t)__shfl((int)outb, max(p, 0));
             const uint32_t b = isrun ? (p < 0 ? front0 : fb) : outb;
@@ -575,6 +602,9 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             if (nblock + total > cap) { flag = kHost; break; }
             const uint32_t at = nblock + incl - cnt;
+#if LFM_BZD_PROBE >= 2  // timing probe (wrong output): no stores
+            if (nblock > cap) 
+#endif
             if (isnorm || (isrun && cnt <= 8u))
                 for (uint32_t q = 0; q < cnt; ++q) ll[at + q] = (uint8_t)b;
             for (uint64_t big = __ballot(isrun && cnt > 8u); big; big &= big - 1) {  // long stretches: all lanes
@@ -596,6 +626,9 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
         const uint32_t ccrc = br.get(32);
         if (ccrc != bcrc) { flag = kHost; break; }  // one block: combined CRC = rotl(0, 1) ^ blockCRC
     } while (false);
+#if LFM_BZD_PROBE
+    if (flag) flag = kCrcFail;  // (never the host library: the probes' streams are not decoded)
+#endif
     if (lane == 0) {
         D.flags[s] = flag;
         D.n[s] = flag ? 0u : nblock;
@@ -1123,6 +1156,18 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
                                       uint32_t out_stride, void* d_ws, size_t ws_bytes, uint32_t* h_lens,
                                       uint32_t* h_flags, void* stream_)
 {
+    const int rc = lfm_hip_bunzip2_issue(d_payload, h_offs, count, d_out, out_stride, d_ws, ws_bytes, h_lens, h_flags,
+                                         stream_);
+    if (rc != LFM_HIP_OK) return rc;
+    return hipStreamSynchronize((hipStream_t)stream_) == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
+}
+
+// the same, returning once the kernels and the copies of h_lens / h_flags
+// (pinned host memory: the copies are asynchronous) are queued on the stream
+extern "C" int lfm_hip_bunzip2_issue(const void* d_payload, const uint64_t* h_offs, uint32_t count, void* d_out,
+                                     uint32_t out_stride, void* d_ws, size_t ws_bytes, uint32_t* h_lens,
+                                     uint32_t* h_flags, void* stream_)
+{
     hipStream_t st = (hipStream_t)stream_;
     if (!d_payload || !h_offs || !count || !d_out || !out_stride || !d_ws) return LFM_HIP_EINVAL;
     if (ws_bytes < lfm_hip_bunzip2_workspace_bytes(count, out_stride) || ((uintptr_t)d_payload & 3)) return LFM_HIP_EINVAL;
@@ -1236,8 +1281,7 @@ extern "C" int lfm_hip_bunzip2_blocks(const void* d_payload, const uint64_t* h_o
     hipLaunchKernelGGL(bzd_rle1, dim3(count), dim3(64), 0, st, D);
     if (hipGetLastError() != hipSuccess) return LFM_HIP_ERUNTIME;
     if (hipMemcpyAsync(h_lens, D.out_len, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(h_flags, D.flags, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
+        hipMemcpyAsync(h_flags, D.flags, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
     return LFM_HIP_OK;
 }

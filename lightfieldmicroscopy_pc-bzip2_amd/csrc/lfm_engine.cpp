@@ -1887,6 +1887,60 @@ bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
     return ok;
 }
 
+// Device -> host through the pinned chunks with the DMA on an SDMA engine:
+// the engine copies chunk i + 1 while the host threads copy chunk i out (the
+// blit kernel of hipMemcpyAsync would run on the CUs beside the next decode
+// chunk's kernels).  The source must be complete (the caller synchronised its
+// stream).  Returns false if HSA cannot take the copy before anything was
+// issued (the caller falls back); a failure after that is reported as false too.
+bool sdma_staged_d2h(void* h_dst, const void* d_src, size_t n, int threads)
+{
+    const hsa_agent_t* cpu = hsa_cpu_agent();
+    Staging& S = staging();
+    if (!cpu || !S.ready() || n == 0) return false;
+    hsa_amd_pointer_info_t info;
+    std::memset(&info, 0, sizeof(info));
+    info.size = sizeof(info);
+    if (hsa_amd_pointer_info((void*)d_src, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        info.type != HSA_EXT_POINTER_TYPE_HSA)
+        return false;
+    hsa_signal_t sig[2];
+    if (hsa_signal_create(0, 0, nullptr, &sig[0]) != HSA_STATUS_SUCCESS) return false;
+    if (hsa_signal_create(0, 0, nullptr, &sig[1]) != HSA_STATUS_SUCCESS) {
+        hsa_signal_destroy(sig[0]);
+        return false;
+    }
+    const size_t nc = (n + Staging::kChunk - 1) / Staging::kChunk;
+    auto issue = [&](size_t i) {
+        const int b = (int)(i & 1);
+        const size_t off = i * Staging::kChunk, len = std::min(Staging::kChunk, n - off);
+        hsa_signal_store_relaxed(sig[b], 1);
+        if (hsa_amd_memory_async_copy(S.buf[b], *cpu, (const uint8_t*)d_src + off, info.agentOwner, len, 0, nullptr,
+                                      sig[b]) != HSA_STATUS_SUCCESS) {
+            hsa_signal_store_relaxed(sig[b], 0);
+            return false;
+        }
+        return true;
+    };
+    auto wait = [&](int b) {
+        return hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) == 0;
+    };
+    bool ok = issue(0);
+    for (size_t i = 0; ok && i < nc; ++i) {
+        const int b = (int)(i & 1);
+        if (i + 1 < nc) ok = issue(i + 1);
+        if (!wait(b)) ok = false;
+        if (!ok) break;
+        const size_t off = i * Staging::kChunk, len = std::min(Staging::kChunk, n - off);
+        par_memcpy_impl((uint8_t*)h_dst + off, S.buf[b], len, threads);
+    }
+    for (int b = 0; b < 2; ++b) (void)wait(b);  // nothing still writes a chunk
+    hsa_signal_destroy(sig[0]);
+    hsa_signal_destroy(sig[1]);
+    S.used[0] = S.used[1] = false;
+    return ok;
+}
+
 bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads)
 {
     Staging& S = staging();
@@ -1913,16 +1967,21 @@ bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int th
     return true;
 }
 
-// Device buffers and stream of the GPU decode, kept per host thread and
-// device between calls (LFM_DECODE_KEEP=0 releases them after every call):
-// fresh device allocations are cleared by the driver before first use, which
-// showed up as 20-40 ms stalls of the first upload.
+// Device buffers, streams and pinned status arrays of the GPU decode, kept
+// per host thread and device between calls (LFM_DECODE_KEEP=0 releases them
+// after every call): fresh device allocations are cleared by the driver
+// before first use, which showed up as 20-40 ms stalls of the first upload.
+// Two slots (stream, workspace, block buffer, lens / flags) for the pipelined
+// chunks of gpu_decode.
 struct DecodeBuffers {
-    enum { PAY, WS, BLK, SYM, OUT, N };
+    enum { PAY, SYM, OUT, WS0, WS1, BLK0, BLK1, N };
     int dev = -1;
-    hipStream_t st = nullptr;
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};  // a slot's inverse predictor done (video hand-over)
     void* p[N] = {};
     size_t cap[N] = {};
+    uint32_t* hs[2] = {nullptr, nullptr};  // pinned: lens then flags, per slot
+    size_t hs_cap[2] = {0, 0};
     DecodeBuffers() = default;
     DecodeBuffers(const DecodeBuffers&) = delete;
     DecodeBuffers& operator=(const DecodeBuffers&) = delete;
@@ -1934,8 +1993,15 @@ struct DecodeBuffers {
             p[i] = nullptr;
             cap[i] = 0;
         }
-        if (st) (void)hipStreamDestroy(st);
-        st = nullptr;
+        for (int k = 0; k < 2; ++k) {
+            if (hs[k]) (void)hipHostFree(hs[k]);
+            hs[k] = nullptr;
+            hs_cap[k] = 0;
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+            ev[k] = nullptr;
+            if (st[k]) (void)hipStreamDestroy(st[k]);
+            st[k] = nullptr;
+        }
         dev = -1;
     }
     bool begin()
@@ -1944,10 +2010,12 @@ struct DecodeBuffers {
         if (hipGetDevice(&d) != hipSuccess) return false;
         if (dev != d) {
             release();
-            if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-                st = nullptr;
-                return false;
-            }
+            for (int k = 0; k < 2; ++k)
+                if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+                    release();
+                    return false;
+                }
             dev = d;
         }
         return true;
@@ -1966,6 +2034,19 @@ struct DecodeBuffers {
         cap[i] = bytes;
         return p[i];
     }
+    uint32_t* status(int k, size_t count)  // 2 * count words: lens, flags
+    {
+        if (hs_cap[k] >= count) return hs[k];
+        if (hs[k]) (void)hipHostFree(hs[k]);
+        hs[k] = nullptr;
+        hs_cap[k] = 0;
+        if (hipHostMalloc((void**)&hs[k], count * 8, hipHostMallocDefault) != hipSuccess) {
+            hs[k] = nullptr;
+            return nullptr;
+        }
+        hs_cap[k] = count;
+        return hs[k];
+    }
 };
 
 DecodeBuffers& decode_buffers()
@@ -1977,10 +2058,16 @@ DecodeBuffers& decode_buffers()
 
 void par_memcpy(void* dst, const void* src, size_t n, int threads) { par_memcpy_impl(dst, src, n, threads); }
 
-// GPU decode of a BZIP2 payload (lfm_bunzip2.hip): payload up, streams decoded
-// in batches into the device image (the few flagged streams by the host
-// library), inverse predictor on the device, image down.  Returns -1 when the
-// GPU path does not apply (the caller decodes on the host).
+// GPU decode of a BZIP2 payload (lfm_bunzip2.hip), pipelined over chunks of
+// whole block slabs (the blocks of one z-block row of one volume, so a chunk's
+// pixels are a contiguous run of frames of the image): per chunk the payload
+// bytes go up (SDMA), its streams are decoded (the few flagged ones by the
+// host library), scattered into the device symbol image, run through the
+// inverse predictor and come down (SDMA) into the caller's image.  Chunks
+// alternate between two HIP streams, and the host works one chunk behind the
+// device: while chunk c's kernels run, chunk c - 1 is finished and copied
+// down and chunk c + 1's payload goes up.  Returns -1 when the GPU path does
+// not apply (the caller decodes on the host).
 static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header& h, uint8_t* img, int family,
                       bool predicted, int k, int video, int threads)
 {
@@ -1989,19 +2076,12 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     const size_t bpp = h.getBytesPerPixel();
     const uint32_t block_bytes = h.getBlockSizeBytes();
     if (!nb || !block_bytes || nb >= (1ull << 31)) return -1;
-    // LFM_DECODE_TIMING=1: phase times on stderr (synchronizes between phases)
+    // LFM_DECODE_TIMING=1: stage times on stderr
     static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
-    auto tp = std::chrono::steady_clock::now();
-    DecodeBuffers& DB = decode_buffers();
-    hipStream_t st = nullptr;
-    auto phase = [&](const char* name) {
-        if (!timing) return;
-        if (st) (void)hipStreamSynchronize(st);
-        const auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "decode phase %-10s %8.2f ms\n", name,
-                     std::chrono::duration<double, std::milli>(now - tp).count());
-        tp = now;
-    };
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    const auto t_start = clk::now();
+    double t_up = 0, t_wait = 0, t_down = 0, t_host = 0;
     std::vector<uint64_t> offs(nb + 1);
     for (uint64_t i = 0; i < nb; ++i) {
         offs[i] = h.getBlockOffset(i);
@@ -2010,112 +2090,173 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     offs[nb] = offs[nb - 1] + h.getBlockCompressedSizeBytes(nb - 1);
     if (offs[nb] > len) return 3;
     const size_t img_bytes = h.getImageSizeBytes();
+    const uint64_t W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
+    const size_t frame_bytes = (size_t)W * H * bpp;
+    // chunks: whole slabs, about LFM_DECODE_CHUNK_BLOCKS blocks each (default
+    // 2048: the 3 872 streams of config 3 in two chunks, config 5's 7 396 per
+    // volume in two per volume); 0 = one chunk
+    const uint64_t slab = g.nb[0] * g.nb[1], nslabs = nb / slab;
+    const long target = env_int("LFM_DECODE_CHUNK_BLOCKS", 2048);
+    uint64_t spc = nslabs;  // slabs per chunk
+    if (target > 0) {
+        const uint64_t want = std::max<uint64_t>(1, (nb + (uint64_t)target - 1) / (uint64_t)target);
+        spc = (nslabs + want - 1) / want;
+    }
     const size_t per = lfm_hip_bunzip2_workspace_bytes(1, block_bytes) + block_bytes;
     const size_t budget = (size_t)env_int("LFM_BUNZIP2_GPU_BUDGET_MB", 16 * 1024) << 20;
-    const uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>(nb, budget / per));
+    spc = std::max<uint64_t>(1, std::min<uint64_t>(spc, budget / 2 / per / slab));
+    const uint64_t batch = spc * slab, nch = (nslabs + spc - 1) / spc;
     const size_t ws = lfm_hip_bunzip2_workspace_bytes((uint32_t)batch, block_bytes);
     static const bool keep = env_int("LFM_DECODE_KEEP", 1) != 0;
+    DecodeBuffers& DB = decode_buffers();
     auto release = [&]() {
         if (!keep) {
             DB.release();
             staging().release();
         }
     };
-    void *d_pay = nullptr, *d_ws = nullptr, *d_blk = nullptr, *d_sym = nullptr, *d_out = nullptr;
+    void *d_pay = nullptr, *d_sym = nullptr, *d_out = nullptr, *d_ws[2] = {}, *d_blk[2] = {};
+    uint32_t* hs[2] = {};
     if (DB.begin()) {
-        st = DB.st;
         d_pay = DB.get(DecodeBuffers::PAY, offs[nb] + 64);
-        d_ws = DB.get(DecodeBuffers::WS, ws);
-        d_blk = DB.get(DecodeBuffers::BLK, batch * block_bytes);
         d_sym = DB.get(DecodeBuffers::SYM, img_bytes);
         d_out = predicted ? DB.get(DecodeBuffers::OUT, img_bytes) : nullptr;
+        for (int q = 0; q < (nch > 1 ? 2 : 1); ++q) {
+            d_ws[q] = DB.get(DecodeBuffers::WS0 + q, ws);
+            d_blk[q] = DB.get(DecodeBuffers::BLK0 + q, batch * block_bytes);
+            hs[q] = DB.status(q, batch);
+        }
     }
-    if (!st || !d_pay || !d_ws || !d_blk || !d_sym || (predicted && !d_out)) {
+    const int nslot = nch > 1 ? 2 : 1;
+    bool have = DB.st[0] && d_pay && d_sym && (!predicted || d_out);
+    for (int q = 0; q < nslot; ++q) have = have && d_ws[q] && d_blk[q] && hs[q];
+    if (!have) {
         DB.release();
         return -1;
     }
-    phase("alloc");
-    int rc = 0;
-    // the payload upload: blit-kernel copies (the runtime's pageable path or
-    // hipMemcpyAsync from the pinned chunks) took 5-47 ms for config 3's
-    // 277 MB depending on the process's state; an SDMA engine does not
-    // LFM_DECODE_H2D: 0 SDMA engine through the pinned chunks (default;
-    // falls back to 1 when HSA cannot take it), 1 one runtime copy, 2 the
-    // pinned chunks with hipMemcpyAsync
-    static const int up_mode = env_int("LFM_DECODE_H2D", 0);
-    bool up_ok = false;
-    if (up_mode == 0) {
-        up_ok = hipStreamSynchronize(st) == hipSuccess && sdma_staged_h2d(d_pay, payload, offs[nb], threads);
-        if (!up_ok) (void)hipGetLastError();
-    }
-    if (!up_ok)
-        up_ok = up_mode == 2 ? staged_h2d(d_pay, payload, offs[nb], st, threads)
-                             : hipMemcpyAsync(d_pay, payload, offs[nb], hipMemcpyHostToDevice, st) == hipSuccess;
-    if (!up_ok ||
-        hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, st) != hipSuccess)
-        rc = 3;
-    phase("upload");
+    const auto t_alloc = clk::now();
     uint32_t dims[5], bs[5];
     for (int d = 0; d < 5; ++d) {
         dims[d] = h.xyzct[d];
         bs[d] = (uint32_t)g.bs[d];
     }
-    std::vector<uint32_t> lens(batch), flags(batch);
+    // payload upload: the SDMA engine through the pinned chunks (LFM_DECODE_H2D
+    // = 0, default; falls back to 1 when HSA cannot take it), 1 one runtime
+    // copy, 2 the pinned chunks with hipMemcpyAsync -- the blit-kernel copies
+    // took 5-47 ms for config 3's 277 MB depending on the process's state
+    static const int up_mode = env_int("LFM_DECODE_H2D", 0);
+    auto upload = [&](uint64_t lo, uint64_t hi, hipStream_t st) {  // payload bytes [lo, hi)
+        lo &= ~(uint64_t)3;  // (4-byte aligned pieces; neighbours rewrite the same bytes)
+        const size_t n = hi - lo;
+        if (up_mode == 0 && sdma_staged_h2d((uint8_t*)d_pay + lo, payload + lo, n, threads)) return true;
+        (void)hipGetLastError();
+        const bool ok = up_mode == 2 ? staged_h2d((uint8_t*)d_pay + lo, payload + lo, n, st, threads)
+                                     : hipMemcpyAsync((uint8_t*)d_pay + lo, payload + lo, n, hipMemcpyHostToDevice,
+                                                      st) == hipSuccess;
+        return ok && hipStreamSynchronize(st) == hipSuccess;
+    };
+    // the frames (volume-major) a chunk's slabs cover: [f0, f1)
+    const uint64_t nbz = g.nb[2];
+    auto frames = [&](uint64_t c, uint64_t& f0, uint64_t& f1) {
+        const uint64_t s0 = c * spc, s1 = std::min(nslabs, s0 + spc) - 1;
+        f0 = (s0 / nbz) * Z + (s0 % nbz) * g.bs[2];
+        f1 = (s1 / nbz) * Z + std::min<uint64_t>(Z, (s1 % nbz + 1) * g.bs[2]);
+    };
     std::vector<uint8_t> hb(block_bytes);
-    for (uint64_t b0 = 0; b0 < nb && !rc; b0 += batch) {
-        const uint32_t cnt = (uint32_t)std::min<uint64_t>(batch, nb - b0);
-        if (lfm_hip_bunzip2_blocks(d_pay, offs.data() + b0, cnt, d_blk, block_bytes, d_ws, ws, lens.data(),
-                                   flags.data(), st) != LFM_HIP_OK) {
-            rc = 3;
-            break;
-        }
-        phase("bunzip2");
-        for (uint32_t i = 0; i < cnt && !rc; ++i) {
+    int rc = 0;
+    if (hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, DB.st[0]) != hipSuccess ||
+        hipStreamSynchronize(DB.st[0]) != hipSuccess)
+        rc = 3;
+    // host side of chunk c once its streams are decoded: host-library blocks,
+    // scatter, inverse predictor, download
+    auto finish = [&](uint64_t c) -> int {
+        const int q = (int)(c % nslot);
+        hipStream_t st = DB.st[q];
+        const uint64_t b0 = c * batch, cnt = std::min<uint64_t>(batch, nb - b0);
+        auto t0 = clk::now();
+        if (hipStreamSynchronize(st) != hipSuccess) return 3;
+        auto t1 = clk::now();
+        t_wait += ms(t0, t1);
+        const uint32_t* lens = hs[q];
+        const uint32_t* flags = hs[q] + batch;
+        for (uint64_t i = 0; i < cnt; ++i) {
             uint64_t o[5], sz[5];
             g.block(b0 + i, o, sz);
             const uint64_t expect = bpp * sz[0] * sz[1] * sz[2] * sz[3] * sz[4];
             if (flags[i] == 1) {  // the host library decodes this stream
                 const int r = decompress_one(BZIP2, payload + offs[b0 + i], (uint32_t)(offs[b0 + i + 1] - offs[b0 + i]),
                                              hb.data(), (uint32_t)expect);
-                if (r) rc = r;
-                else if (hipMemcpyAsync((uint8_t*)d_blk + (size_t)i * block_bytes, hb.data(), expect,
-                                        hipMemcpyHostToDevice, st) != hipSuccess ||
-                         hipStreamSynchronize(st) != hipSuccess)
-                    rc = 3;
+                if (r) return r;
+                if (hipMemcpyAsync((uint8_t*)d_blk[q] + (size_t)i * block_bytes, hb.data(), expect,
+                                   hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess)
+                    return 3;
             } else if (flags[i] != 0 || lens[i] != expect) {
                 std::printf("ERROR: block %llu of the payload does not decode to its %llu bytes (bzip2 CRC / length)\n",
                             (unsigned long long)(b0 + i), (unsigned long long)expect);
-                rc = 2;
+                return 2;
             }
         }
-        if (!rc && lfm_hip_scatter_blocks(d_blk, block_bytes, (uint32_t)b0, cnt, dims, bs, (uint32_t)bpp, d_sym, st) !=
-                       LFM_HIP_OK)
+        if (lfm_hip_scatter_blocks(d_blk[q], block_bytes, (uint32_t)b0, (uint32_t)cnt, dims, bs, (uint32_t)bpp, d_sym,
+                                   st) != LFM_HIP_OK)
+            return 3;
+        uint64_t f0, f1;
+        frames(c, f0, f1);
+        if (predicted) {
+            // a temporal first frame (video, odd z) reads the previous chunk's
+            // last decoded frame: wait for that chunk's inverse predictor
+            if (video && c > 0 && hipStreamWaitEvent(st, DB.ev[(c - 1) % nslot], 0) != hipSuccess) return 3;
+            for (uint64_t f = f0; f < f1;) {  // per volume
+                const uint64_t v = f / Z, z0 = f % Z, n = std::min<uint64_t>(f1, (v + 1) * Z) - f;
+                const uint16_t* prev = z0 > 0 ? (const uint16_t*)d_out + (f - 1) * W * H : nullptr;
+                const int hr = lfm_hip_unpredict((const uint16_t*)d_sym + f * W * H, prev, (uint16_t*)d_out + f * W * H,
+                                                 (int)W, (int)H, (int)n, h.Nnum, family, k, video, (int)z0, st);
+                if (hr == LFM_HIP_ENOTINV) {
+                    std::printf("ERROR: frames of this file cannot be inverted (temporal angle/space predictor)\n");
+                    return 3;
+                }
+                if (hr != LFM_HIP_OK) return 3;
+                f += n;
+            }
+            if (hipEventRecord(DB.ev[q], st) != hipSuccess) return 3;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) return 3;
+        auto t2 = clk::now();
+        t_host += ms(t1, t2);
+        const size_t o0 = f0 * frame_bytes, n = (f1 - f0) * frame_bytes;
+        const uint8_t* src = (const uint8_t*)(predicted ? d_out : d_sym) + o0;
+        if (!sdma_staged_d2h(img + o0, src, n, threads) && !staged_d2h(img + o0, src, n, st, threads)) return 3;
+        if (hipStreamSynchronize(st) != hipSuccess) return 3;
+        t_down += ms(t2, clk::now());
+        return 0;
+    };
+    for (uint64_t c = 0; c < nch && !rc; ++c) {
+        const int q = (int)(c % nslot);
+        const uint64_t b0 = c * batch, cnt = std::min<uint64_t>(batch, nb - b0);
+        auto t0 = clk::now();
+        if (!upload(offs[b0], offs[b0 + cnt], DB.st[q])) {
             rc = 3;
-    }
-    phase("scatter");
-    if (!rc && predicted) {
-        const int W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
-        const uint64_t V = (uint64_t)h.xyzct[3] * h.xyzct[4];
-        const size_t vb = (size_t)W * H * Z * 2;
-        for (uint64_t v = 0; v < V && !rc; ++v) {
-            const int hr = lfm_hip_unpredict((const uint16_t*)((uint8_t*)d_sym + v * vb), nullptr,
-                                             (uint16_t*)((uint8_t*)d_out + v * vb), W, H, Z, h.Nnum, family, k, video,
-                                             0, st);
-            if (hr == LFM_HIP_ENOTINV) {
-                std::printf("ERROR: frames of this file cannot be inverted (temporal angle/space predictor)\n");
-                rc = 3;
-            } else if (hr != LFM_HIP_OK) {
-                rc = 3;
-            }
+            break;
         }
+        t_up += ms(t0, clk::now());
+        if (lfm_hip_bunzip2_issue(d_pay, offs.data() + b0, (uint32_t)cnt, d_blk[q], block_bytes, d_ws[q], ws, hs[q],
+                                  hs[q] + batch, DB.st[q]) != LFM_HIP_OK) {
+            rc = 3;
+            break;
+        }
+        if (c > 0) rc = finish(c - 1);
     }
-    phase("unpredict");
-    if (!rc && (!staged_d2h(img, predicted ? d_out : d_sym, img_bytes, st, threads) ||
-                hipStreamSynchronize(st) != hipSuccess))
-        rc = 3;
-    phase("download");
+    if (!rc) rc = finish(nch - 1);
+    if (rc) {  // nothing may still run on the buffers
+        for (int q = 0; q < nslot; ++q) (void)hipStreamSynchronize(DB.st[q]);
+    }
+    if (timing)
+        std::fprintf(stderr,
+                     "decode: %llu chunks of <= %llu blocks, alloc %.2f ms, upload %.2f, wait %.2f, host + kernels "
+                     "after wait %.2f, download %.2f, total %.2f ms\n",
+                     (unsigned long long)nch, (unsigned long long)batch, ms(t_start, t_alloc), t_up, t_wait, t_host,
+                     t_down, ms(t_start, clk::now()));
     release();
-    phase("free");
     return rc;
 }
 

@@ -486,11 +486,21 @@ def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):
     return out
 
 
-def decode_roi(buf, lb, ub, dtype=np.uint16, num_threads=-1):
+def decode_roi(buf, lb, ub, dtype=np.uint16, num_threads=-1, out=None):
     """Region lb .. ub (inclusive, [x, y, z, c, t]) of an in-memory .lfm
-    (lfm_decode_memory_roi); returns an array [t, c, z, y, x] of the region."""
+    (lfm_decode_memory_roi); returns an array [t, c, z, y, x] of the region.
+    `out` (optional): a C-contiguous array of the region's size and dtype to
+    decode into (readKLBroiInPlace's caller-owned buffer), returned reshaped."""
     shape = tuple(int(u) - int(l) + 1 for l, u in zip(lb, ub))[::-1]
-    out = np.empty(shape, dtype=dtype)
+    if out is None:
+        out = np.empty(shape, dtype=dtype)
+    else:
+        if not isinstance(out, np.ndarray) or not out.flags.c_contiguous or not out.flags.writeable:
+            raise ValueError("decode_roi: out must be a writeable C-contiguous numpy array")
+        if out.dtype != np.dtype(dtype) or out.size != int(np.prod(shape)):
+            raise ValueError("decode_roi: out holds %d x %s, the region is %s x %s"
+                             % (out.size, out.dtype, shape, np.dtype(dtype)))
+        out = out.reshape(shape)
     _check(lib().lfm_decode_memory_roi(_addr(buf), len(buf), _u32(lb), _u32(ub), out.ctypes.data, num_threads),
            "lfm_decode_memory_roi")
     return out

@@ -211,6 +211,28 @@ def test_roi_reads_match_crop_of_full_decode(lfmlib, tmp_path):
         assert np.array_equal(got, want), (lb, ub)
 
 
+def test_decode_memory_roi_into_caller_buffer(lfmlib):
+    """lfm_decode_memory_roi (lfm.decode_roi) on an in-memory .lfm: whole
+    t-volumes and a sub-box equal the crop of the image, decoded into a fresh
+    array or into a caller buffer reused across calls; a buffer of the wrong
+    size or type is refused before anything is written."""
+    man = _manifest()
+    b = open(os.path.join(GOLDEN, man["imgtif_stack_auto_video"]["file"]), "rb").read()
+    img = _img_tif()
+    Z, Y, X = img.shape
+    whole = lfmlib.decode_roi(b, [0, 0, 0, 0, 0], [X - 1, Y - 1, Z - 1, 0, 0])
+    assert np.array_equal(whole.reshape(img.shape), img)
+    buf = np.zeros((5, 40, 30), np.uint16)
+    for z0 in (0, 3, Z - 5):
+        got = lfmlib.decode_roi(b, [7, 11, z0, 0, 0], [36, 50, z0 + 4, 0, 0], out=buf)
+        assert got.base is buf or got is buf
+        assert np.array_equal(buf, img[z0:z0 + 5, 11:51, 7:37]), z0
+    with pytest.raises(ValueError):
+        lfmlib.decode_roi(b, [0, 0, 0, 0, 0], [9, 9, 0, 0, 0], out=np.zeros((10, 11), np.uint16))
+    with pytest.raises(ValueError):
+        lfmlib.decode_roi(b, [0, 0, 0, 0, 0], [9, 9, 0, 0, 0], out=np.zeros((10, 10), np.int32))
+
+
 def test_invalid_predictor_request_rejected(lfmlib, tmp_path):
     img = np.zeros((1, 16, 16), np.uint16)
     with pytest.raises(lfmlib.LfmError, match="code 6"):
