@@ -1875,12 +1875,13 @@ bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
                                        sig[b]) == HSA_STATUS_SUCCESS;
         if (!ok) hsa_signal_store_relaxed(sig[b], 0);
     }
+    auto t_tail = now();
     for (int b = 0; b < 2; ++b)
         if (hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) != 0)
             ok = false;
     if (timing)
-        std::fprintf(stderr, "sdma h2d: %zu bytes, host copies %.2f ms, waits %.2f ms, %d threads\n", n, t_copy, t_wait,
-                     threads);
+        std::fprintf(stderr, "sdma h2d: %zu bytes, host copies %.2f ms, waits %.2f ms, last copy %.2f ms, %d threads\n",
+                     n, t_copy, t_wait, std::chrono::duration<double, std::milli>(now() - t_tail).count(), threads);
     hsa_signal_destroy(sig[0]);
     hsa_signal_destroy(sig[1]);
     S.used[0] = S.used[1] = false;  // the chunks are free (no HIP event pending on them)
@@ -2239,6 +2240,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             break;
         }
         t_up += ms(t0, clk::now());
+        if (timing) std::fprintf(stderr, "decode: chunk %llu upload %.2f ms\n", (unsigned long long)c, ms(t0, clk::now()));
         if (lfm_hip_bunzip2_issue(d_pay, offs.data() + b0, (uint32_t)cnt, d_blk[q], block_bytes, d_ws[q], ws, hs[q],
                                   hs[q] + batch, DB.st[q]) != LFM_HIP_OK) {
             rc = 3;
