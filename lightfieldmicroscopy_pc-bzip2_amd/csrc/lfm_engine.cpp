@@ -2093,15 +2093,18 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     const size_t img_bytes = h.getImageSizeBytes();
     const uint64_t W = h.xyzct[0], H = h.xyzct[1], Z = h.xyzct[2];
     const size_t frame_bytes = (size_t)W * H * bpp;
-    // chunks: whole slabs, about LFM_DECODE_CHUNK_BLOCKS blocks each (default
-    // 2048: the 3 872 streams of config 3 in two chunks, config 5's 7 396 per
-    // volume in two per volume); 0 = one chunk
+    // chunks: whole slabs, at least two and about LFM_DECODE_CHUNK_BLOCKS
+    // blocks each (default 4096, about the streams the Huffman kernel holds
+    // resident at once: config 3's 3 872 streams in two chunks, a config-5
+    // volume's 7 396 in two); 0 = one chunk.  With two slots a third chunk
+    // cannot start before the first is finished, so smaller chunks lose (four
+    // chunks of 968 streams: 75.6 vs 54.3 ms on config 3)
     const uint64_t slab = g.nb[0] * g.nb[1], nslabs = nb / slab;
-    const long target = env_int("LFM_DECODE_CHUNK_BLOCKS", 2048);
+    const long target = env_int("LFM_DECODE_CHUNK_BLOCKS", 4096);
     uint64_t spc = nslabs;  // slabs per chunk
     if (target > 0) {
-        const uint64_t want = std::max<uint64_t>(1, (nb + (uint64_t)target - 1) / (uint64_t)target);
-        spc = (nslabs + want - 1) / want;
+        const uint64_t want = std::max<uint64_t>(2, (nb + (uint64_t)target - 1) / (uint64_t)target);
+        spc = std::max<uint64_t>(1, (nslabs + want - 1) / want);
     }
     const size_t per = lfm_hip_bunzip2_workspace_bytes(1, block_bytes) + block_bytes;
     const size_t budget = (size_t)env_int("LFM_BUNZIP2_GPU_BUDGET_MB", 16 * 1024) << 20;
@@ -2422,18 +2425,30 @@ int decode_roi(const uint8_t* payload, size_t len, const klb_image_header& h, co
                         sub.blockOffset[ids.size()] = total;
                         ids.push_back(id);
                     }
-    std::vector<uint8_t> spay(total);
-    parallel_for(ids.size(), threads, [&](uint64_t i) {
-        const uint64_t id = ids[i], sz = h.getBlockCompressedSizeBytes(id);
-        std::memcpy(spay.data() + (sub.blockOffset[i] - sz), payload + h.getBlockOffset(id), sz);
-    });
+    // the region's streams: a run of consecutive blocks (whole t-volumes, a
+    // z-range of whole frames) is read where it lies in the payload; anything
+    // else is gathered into a buffer (no zero fill: every byte is copied)
+    bool run = true;
+    for (size_t i = 1; i < ids.size() && run; ++i)
+        run = ids[i] == ids[i - 1] + 1 && h.getBlockOffset(ids[i]) == h.getBlockOffset(ids[i - 1]) +
+                                                                         h.getBlockCompressedSizeBytes(ids[i - 1]);
+    std::unique_ptr<uint8_t[]> gathered;
+    const uint8_t* spay = ids.empty() ? payload : payload + h.getBlockOffset(ids[0]);
+    if (!run) {
+        gathered.reset(new uint8_t[total]);
+        parallel_for(ids.size(), threads, [&](uint64_t i) {
+            const uint64_t id = ids[i], sz = h.getBlockCompressedSizeBytes(id);
+            std::memcpy(gathered.get() + (sub.blockOffset[i] - sz), payload + h.getBlockOffset(id), sz);
+        });
+        spay = gathered.get();
+    }
     // a region that is exactly its blocks' box (e.g. whole t-volumes) is
     // decoded straight into `out`: no temporary image, no crop
     bool exact = true;
     for (int d = 0; d < 5; ++d) exact = exact && o[d] == lb[d] && n[d] == (uint64_t)ub[d] - lb[d] + 1;
-    if (exact) return decode_payload(spay.data(), spay.size(), sub, out, threads, family);
+    if (exact) return decode_payload(spay, total, sub, out, threads, family);
     std::unique_ptr<uint8_t[]> simg(new uint8_t[sub.getImageSizeBytes()]);  // (no zero fill: every byte is decoded)
-    const int rc = decode_payload(spay.data(), spay.size(), sub, simg.get(), threads, family);
+    const int rc = decode_payload(spay, total, sub, simg.get(), threads, family);
     if (rc) return rc;
     const size_t row = (size_t)(ub[0] - lb[0] + 1) * bpp;
     const uint64_t ny = (uint64_t)ub[1] - lb[1] + 1, nz = (uint64_t)ub[2] - lb[2] + 1, nc = (uint64_t)ub[3] - lb[3] + 1;
