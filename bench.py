@@ -361,10 +361,16 @@ def config5_host_leg(local, threads, nvol):
         # one untimed volume first: device buffers, pinned staging and the
         # writer's threads are set up once per process, as in a long acquisition
         enc.encode_multi(img[:1], header_version=0x80, nnum=T5, copy=True)
-        t0 = time.perf_counter()
-        b, st = enc.encode_multi(img, header_version=0x80, nnum=T5, copy=False)
-        enc_s = time.perf_counter() - t0
-        print("config5_host: encoded in %.2f s" % enc_s, file=sys.stderr, flush=True)
+        # two timed calls: the first also allocates and first-touches the
+        # device buffers for the whole stack; the second is the steady state
+        # of a writer that is called again with stacks of the same shape
+        enc_runs = []
+        for _ in range(2):
+            t0 = time.perf_counter()
+            b, st = enc.encode_multi(img, header_version=0x80, nnum=T5, copy=False)
+            enc_runs.append(time.perf_counter() - t0)
+            print("config5_host: encoded in %.2f s" % enc_runs[-1], file=sys.stderr, flush=True)
+        enc_s = enc_runs[-1]
         nb = 4 * 43 * 43  # blocks per volume (96 x 96 x 8)
         offs = np.frombuffer(b, dtype="<u8", count=nvol * nb, offset=320)
         base, prev, sha_ok = 320 + 8 * nvol * nb, 0, None
@@ -393,6 +399,7 @@ def config5_host_leg(local, threads, nvol):
         lfm.release_encoders()
         lfm.set_family(FAMILY)
     out.update({"volumes": nvol, "encode_Mpixel_per_s": round(px / enc_s / 1e6, 1), "encode_s": round(enc_s, 3),
+                "encode_first_call_s": round(enc_runs[0], 3),
                 "h2d_ms": round(st["h2d_ms"], 1), "ratio": round(px * 2 / lfm_bytes, 4),
                 "verified": {"against": "cfg5x4 per-volume SHA-256 of volumes 0..%d (oracle, reference bzip2-1.0.6)"
                                         % (min(4, nvol) - 1), "ok": sha_ok},

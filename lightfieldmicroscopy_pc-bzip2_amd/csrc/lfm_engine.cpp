@@ -1789,6 +1789,85 @@ Staging& staging()
     return s;
 }
 
+// Multi-threaded memcpy on a persistent pool: the staged copies run one
+// 32 MiB chunk at a time, and starting and joining 15 threads per chunk
+// (parallel_for) cost about as much as the copy.  A copy is split into 1 MiB
+// pieces that the caller and up to threads - 1 pool workers take in turn;
+// several callers (the decode's upload and download threads) share the pool.
+// The pool is never destroyed (its workers may still wait on it at exit).
+struct CopyPool {
+    struct Job {
+        uint8_t* dst;
+        const uint8_t* src;
+        size_t n, piece;
+        uint64_t np;
+        int helpers;                      // pool workers still allowed to join
+        int active = 0;                   // pool workers inside run() (under mu)
+        std::atomic<uint64_t> next{0}, done{0};
+    };
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<Job*> jobs;
+    int nthreads = 0;
+    static void run(Job& j)
+    {
+        for (;;) {
+            const uint64_t i = j.next.fetch_add(1);
+            if (i >= j.np) return;
+            const size_t o = i * j.piece;
+            std::memcpy(j.dst + o, j.src + o, std::min(j.piece, j.n - o));
+            j.done.fetch_add(1);
+        }
+    }
+    void worker()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return !jobs.empty(); });
+            Job* j = nullptr;
+            for (Job* c : jobs)
+                if (c->helpers > 0 && c->next.load() < c->np) {
+                    j = c;
+                    break;
+                }
+            if (!j) {  // every queued job is fully handed out: wait for the next one
+                cv.wait(lk);
+                continue;
+            }
+            --j->helpers;
+            ++j->active;
+            lk.unlock();
+            run(*j);
+            lk.lock();
+            --j->active;  // (the last touch of the job: its owner waits for this under mu)
+            done_cv.notify_all();
+        }
+    }
+    void copy(void* dst, const void* src, size_t n, int threads)
+    {
+        Job j;
+        j.dst = (uint8_t*)dst;
+        j.src = (const uint8_t*)src;
+        j.n = n;
+        j.piece = 1u << 20;
+        j.np = (n + j.piece - 1) / j.piece;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            while (nthreads < threads - 1) {
+                std::thread(&CopyPool::worker, this).detach();
+                ++nthreads;
+            }
+            j.helpers = (int)std::min<uint64_t>((uint64_t)threads - 1, j.np - 1);
+            jobs.push_back(&j);
+        }
+        cv.notify_all();
+        run(j);
+        std::unique_lock<std::mutex> lk(mu);
+        done_cv.wait(lk, [&] { return j.done.load() == j.np && j.active == 0; });
+        jobs.erase(std::find(jobs.begin(), jobs.end(), &j));
+    }
+};
+
 void par_memcpy_impl(void* dst, const void* src, size_t n, int threads)
 {
     const size_t piece = 1u << 20;
@@ -1797,10 +1876,8 @@ void par_memcpy_impl(void* dst, const void* src, size_t n, int threads)
         std::memcpy(dst, src, n);
         return;
     }
-    parallel_for(np, threads, [&](uint64_t i) {
-        const size_t o = i * piece;
-        std::memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(piece, n - o));
-    });
+    static CopyPool* pool = new CopyPool;  // (never destroyed, see CopyPool)
+    pool->copy(dst, src, n, std::min(threads, 64));
 }
 
 bool staged_h2d(void* d_dst, const void* h_src, size_t n, hipStream_t st, int threads)
@@ -1894,10 +1971,9 @@ bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
 // chunk's kernels).  The source must be complete (the caller synchronised its
 // stream).  Returns false if HSA cannot take the copy before anything was
 // issued (the caller falls back); a failure after that is reported as false too.
-bool sdma_staged_d2h(void* h_dst, const void* d_src, size_t n, int threads)
+bool sdma_staged_d2h(void* h_dst, const void* d_src, size_t n, int threads, Staging& S)
 {
     const hsa_agent_t* cpu = hsa_cpu_agent();
-    Staging& S = staging();
     if (!cpu || !S.ready() || n == 0) return false;
     hsa_amd_pointer_info_t info;
     std::memset(&info, 0, sizeof(info));
@@ -1942,9 +2018,8 @@ bool sdma_staged_d2h(void* h_dst, const void* d_src, size_t n, int threads)
     return ok;
 }
 
-bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads)
+bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads, Staging& S)
 {
-    Staging& S = staging();
     if (!S.ready())
         return hipMemcpyAsync(h_dst, d_src, n, hipMemcpyDeviceToHost, st) == hipSuccess &&
                hipStreamSynchronize(st) == hipSuccess;
@@ -1968,6 +2043,11 @@ bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int th
     return true;
 }
 
+bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads)
+{
+    return staged_d2h(h_dst, d_src, n, st, threads, staging());
+}
+
 // Device buffers, streams and pinned status arrays of the GPU decode, kept
 // per host thread and device between calls (LFM_DECODE_KEEP=0 releases them
 // after every call): fresh device allocations are cleared by the driver
@@ -1983,6 +2063,7 @@ struct DecodeBuffers {
     size_t cap[N] = {};
     uint32_t* hs[2] = {nullptr, nullptr};  // pinned: lens then flags, per slot
     size_t hs_cap[2] = {0, 0};
+    Staging down;                            // the download thread's pinned chunks
     DecodeBuffers() = default;
     DecodeBuffers(const DecodeBuffers&) = delete;
     DecodeBuffers& operator=(const DecodeBuffers&) = delete;
@@ -2003,6 +2084,7 @@ struct DecodeBuffers {
             if (st[k]) (void)hipStreamDestroy(st[k]);
             st[k] = nullptr;
         }
+        down.release();
         dev = -1;
     }
     bool begin()
@@ -2171,8 +2253,12 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     if (hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, DB.st[0]) != hipSuccess ||
         hipStreamSynchronize(DB.st[0]) != hipSuccess)
         rc = 3;
+    // per chunk: its scatter + inverse predictor done (the download waits for it)
+    std::vector<hipEvent_t> cev(nch, nullptr);
+    for (uint64_t c = 0; c < nch && !rc; ++c)
+        if (hipEventCreateWithFlags(&cev[c], hipEventDisableTiming) != hipSuccess) rc = 3;
     // host side of chunk c once its streams are decoded: host-library blocks,
-    // scatter, inverse predictor, download
+    // then scatter and inverse predictor queued behind them (no wait)
     auto finish = [&](uint64_t c) -> int {
         const int q = (int)(c % nslot);
         hipStream_t st = DB.st[q];
@@ -2204,12 +2290,12 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
         if (lfm_hip_scatter_blocks(d_blk[q], block_bytes, (uint32_t)b0, (uint32_t)cnt, dims, bs, (uint32_t)bpp, d_sym,
                                    st) != LFM_HIP_OK)
             return 3;
-        uint64_t f0, f1;
-        frames(c, f0, f1);
         if (predicted) {
+            uint64_t f0, f1;
+            frames(c, f0, f1);
             // a temporal first frame (video, odd z) reads the previous chunk's
             // last decoded frame: wait for that chunk's inverse predictor
-            if (video && c > 0 && hipStreamWaitEvent(st, DB.ev[(c - 1) % nslot], 0) != hipSuccess) return 3;
+            if (video && c > 0 && hipStreamWaitEvent(st, cev[c - 1], 0) != hipSuccess) return 3;
             for (uint64_t f = f0; f < f1;) {  // per volume
                 const uint64_t v = f / Z, z0 = f % Z, n = std::min<uint64_t>(f1, (v + 1) * Z) - f;
                 const uint16_t* prev = z0 > 0 ? (const uint16_t*)d_out + (f - 1) * W * H : nullptr;
@@ -2222,17 +2308,50 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                 if (hr != LFM_HIP_OK) return 3;
                 f += n;
             }
-            if (hipEventRecord(DB.ev[q], st) != hipSuccess) return 3;
         }
-        if (hipStreamSynchronize(st) != hipSuccess) return 3;
-        auto t2 = clk::now();
-        t_host += ms(t1, t2);
-        const size_t o0 = f0 * frame_bytes, n = (f1 - f0) * frame_bytes;
-        const uint8_t* src = (const uint8_t*)(predicted ? d_out : d_sym) + o0;
-        if (!sdma_staged_d2h(img + o0, src, n, threads) && !staged_d2h(img + o0, src, n, st, threads)) return 3;
-        if (hipStreamSynchronize(st) != hipSuccess) return 3;
-        t_down += ms(t2, clk::now());
+        if (hipEventRecord(cev[c], st) != hipSuccess) return 3;
+        t_host += ms(t1, clk::now());
         return 0;
+    };
+    // the downloads run on their own thread (own pinned chunks), in chunk
+    // order, each once its chunk's event fires: the loop below goes on queueing
+    // the next chunks meanwhile
+    std::mutex dmu;
+    std::condition_variable dcv;
+    uint64_t dl_ready = 0;  // chunks [0, dl_ready) may be downloaded
+    bool dl_stop = false;
+    int drc = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::thread downloader([&]() {
+        (void)hipSetDevice(dev);
+        for (uint64_t c = 0; c < nch; ++c) {
+            {
+                std::unique_lock<std::mutex> lk(dmu);
+                dcv.wait(lk, [&] { return dl_ready > c || dl_stop; });
+                if (dl_ready <= c) return;  // stopped
+            }
+            auto t0 = clk::now();
+            uint64_t f0, f1;
+            frames(c, f0, f1);
+            const size_t o0 = f0 * frame_bytes, n = (f1 - f0) * frame_bytes;
+            const uint8_t* src = (const uint8_t*)(predicted ? d_out : d_sym) + o0;
+            hipStream_t st = DB.st[c % nslot];
+            if (hipEventSynchronize(cev[c]) != hipSuccess ||
+                (!sdma_staged_d2h(img + o0, src, n, threads, DB.down) &&
+                 (!staged_d2h(img + o0, src, n, st, threads, DB.down) || hipStreamSynchronize(st) != hipSuccess))) {
+                drc = 3;
+                return;
+            }
+            t_down += ms(t0, clk::now());
+        }
+    });
+    auto hand_over = [&](uint64_t c) {
+        {
+            std::lock_guard<std::mutex> lk(dmu);
+            dl_ready = c + 1;
+        }
+        dcv.notify_all();
     };
     for (uint64_t c = 0; c < nch && !rc; ++c) {
         const int q = (int)(c % nslot);
@@ -2249,12 +2368,23 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             rc = 3;
             break;
         }
-        if (c > 0) rc = finish(c - 1);
+        if (c > 0) {
+            rc = finish(c - 1);
+            if (!rc) hand_over(c - 1);
+        }
     }
     if (!rc) rc = finish(nch - 1);
-    if (rc) {  // nothing may still run on the buffers
-        for (int q = 0; q < nslot; ++q) (void)hipStreamSynchronize(DB.st[q]);
+    if (!rc) hand_over(nch - 1);
+    {
+        std::lock_guard<std::mutex> lk(dmu);
+        dl_stop = true;
     }
+    dcv.notify_all();
+    downloader.join();
+    if (!rc) rc = drc;
+    for (int q = 0; q < nslot; ++q) (void)hipStreamSynchronize(DB.st[q]);  // nothing may still run on the buffers
+    for (hipEvent_t e : cev)
+        if (e) (void)hipEventDestroy(e);
     if (timing)
         std::fprintf(stderr,
                      "decode: %llu chunks of <= %llu blocks, alloc %.2f ms, upload %.2f, wait %.2f, host + kernels "
