@@ -168,7 +168,7 @@ bool PinnedBuffer::reserve(size_t n)
         malloced_ = true;
         return true;
     }
-    if (p_ && size_) std::memcpy(q, p_, size_);
+    if (p_ && size_) par_memcpy(q, p_, size_, default_threads());
     if (p_) {
         if (malloced_) std::free(p_);
         else (void)hipHostFree(p_);

@@ -88,7 +88,16 @@ public:
     int finish(const klb_image_header& h) override;
     bool direct_capable() const override { return true; }
     uint8_t* direct(size_t n) override;
-    void reserve_hint(size_t n) override { (void)out_->reserve(n); }
+    // n is the worst case (every block stored at its raw size + bzip2's
+    // overhead); beyond 8 GiB only 60 % of it is pinned up front (ratio >= 1.67
+    // fits; a worse one grows the buffer by half again, with a copy): a
+    // 100-volume config-5 stack (107 GB raw, 52 GB .lfm) would otherwise pin
+    // 110 GB of host memory for its output
+    void reserve_hint(size_t n) override
+    {
+        const size_t big = (size_t)8 << 30;
+        (void)out_->reserve(n <= big ? n : std::max(big, n / 10 * 6));
+    }
 private:
     PinnedBuffer* out_;
 };
