@@ -2055,14 +2055,14 @@ bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int th
 // Two slots (stream, workspace, block buffer, lens / flags) for the pipelined
 // chunks of gpu_decode.
 struct DecodeBuffers {
-    enum { PAY, SYM, OUT, WS0, WS1, BLK0, BLK1, N };
+    static constexpr int kSlots = 3;
+    enum { PAY, SYM, OUT, WS0, BLK0 = WS0 + kSlots, N = BLK0 + kSlots };
     int dev = -1;
-    hipStream_t st[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};  // a slot's inverse predictor done (video hand-over)
+    hipStream_t st[kSlots] = {};
     void* p[N] = {};
     size_t cap[N] = {};
-    uint32_t* hs[2] = {nullptr, nullptr};  // pinned: lens then flags, per slot
-    size_t hs_cap[2] = {0, 0};
+    uint32_t* hs[kSlots] = {};  // pinned: lens then flags, per slot
+    size_t hs_cap[kSlots] = {};
     Staging down;                            // the download thread's pinned chunks
     DecodeBuffers() = default;
     DecodeBuffers(const DecodeBuffers&) = delete;
@@ -2075,12 +2075,10 @@ struct DecodeBuffers {
             p[i] = nullptr;
             cap[i] = 0;
         }
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kSlots; ++k) {
             if (hs[k]) (void)hipHostFree(hs[k]);
             hs[k] = nullptr;
             hs_cap[k] = 0;
-            if (ev[k]) (void)hipEventDestroy(ev[k]);
-            ev[k] = nullptr;
             if (st[k]) (void)hipStreamDestroy(st[k]);
             st[k] = nullptr;
         }
@@ -2093,9 +2091,8 @@ struct DecodeBuffers {
         if (hipGetDevice(&d) != hipSuccess) return false;
         if (dev != d) {
             release();
-            for (int k = 0; k < 2; ++k)
-                if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+            for (int k = 0; k < kSlots; ++k)
+                if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) {
                     release();
                     return false;
                 }
@@ -2183,14 +2180,15 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     // chunks of 968 streams: 75.6 vs 54.3 ms on config 3)
     const uint64_t slab = g.nb[0] * g.nb[1], nslabs = nb / slab;
     const long target = env_int("LFM_DECODE_CHUNK_BLOCKS", 4096);
+    static const int slots = std::max(2, std::min(env_int("LFM_DECODE_SLOTS", 2), (int)DecodeBuffers::kSlots));
     uint64_t spc = nslabs;  // slabs per chunk
     if (target > 0) {
-        const uint64_t want = std::max<uint64_t>(2, (nb + (uint64_t)target - 1) / (uint64_t)target);
+        const uint64_t want = std::max<uint64_t>(slots, (nb + (uint64_t)target - 1) / (uint64_t)target);
         spc = std::max<uint64_t>(1, (nslabs + want - 1) / want);
     }
     const size_t per = lfm_hip_bunzip2_workspace_bytes(1, block_bytes) + block_bytes;
     const size_t budget = (size_t)env_int("LFM_BUNZIP2_GPU_BUDGET_MB", 16 * 1024) << 20;
-    spc = std::max<uint64_t>(1, std::min<uint64_t>(spc, budget / 2 / per / slab));
+    spc = std::max<uint64_t>(1, std::min<uint64_t>(spc, budget / slots / per / slab));
     const uint64_t batch = spc * slab, nch = (nslabs + spc - 1) / spc;
     const size_t ws = lfm_hip_bunzip2_workspace_bytes((uint32_t)batch, block_bytes);
     static const bool keep = env_int("LFM_DECODE_KEEP", 1) != 0;
@@ -2201,19 +2199,20 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             staging().release();
         }
     };
-    void *d_pay = nullptr, *d_sym = nullptr, *d_out = nullptr, *d_ws[2] = {}, *d_blk[2] = {};
-    uint32_t* hs[2] = {};
+    const int nslot = (int)std::min<uint64_t>(nch, (uint64_t)slots);
+    void *d_pay = nullptr, *d_sym = nullptr, *d_out = nullptr, *d_ws[DecodeBuffers::kSlots] = {},
+         *d_blk[DecodeBuffers::kSlots] = {};
+    uint32_t* hs[DecodeBuffers::kSlots] = {};
     if (DB.begin()) {
         d_pay = DB.get(DecodeBuffers::PAY, offs[nb] + 64);
         d_sym = DB.get(DecodeBuffers::SYM, img_bytes);
         d_out = predicted ? DB.get(DecodeBuffers::OUT, img_bytes) : nullptr;
-        for (int q = 0; q < (nch > 1 ? 2 : 1); ++q) {
+        for (int q = 0; q < nslot; ++q) {
             d_ws[q] = DB.get(DecodeBuffers::WS0 + q, ws);
             d_blk[q] = DB.get(DecodeBuffers::BLK0 + q, batch * block_bytes);
             hs[q] = DB.status(q, batch);
         }
     }
-    const int nslot = nch > 1 ? 2 : 1;
     bool have = DB.st[0] && d_pay && d_sym && (!predicted || d_out);
     for (int q = 0; q < nslot; ++q) have = have && d_ws[q] && d_blk[q] && hs[q];
     if (!have) {
