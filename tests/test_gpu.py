@@ -735,6 +735,8 @@ def test_submit_select_frame_and_wait_codes(lfmlib, oracle, gpu):
         assert enc.wait(t)[0] == exp
         with pytest.raises(lfmlib.LfmError):
             enc.submit(d[8:], z0=8, header_version=0, nnum=15)
+        with pytest.raises(lfmlib.LfmError):  # (the synchronous slab entry refuses it too)
+            enc.encode_slab(d[8:], 8, prev=d[7], header_version=0, nnum=15)
         out = ctypes.POINTER(ctypes.c_uint8)()
         n = ctypes.c_uint64(123)
         rc = lfmlib.lib().lfm_encoder_wait(enc._h, 987654321, ctypes.byref(out), ctypes.byref(n), None)
@@ -764,6 +766,33 @@ def test_decode_path_switches(lfmlib, oracle, gpu, tmp_path, env):
         lfmlib.set_family("tiles")
     out = tmp_path / "out.npy"
     code = ("import sys; sys.path.insert(0, %r); import numpy as np, lfm; lfm.set_family('angle'); "
+            "o, _, _ = lfm.read_lfm(%r); np.save(%r, o)" % (PKG, str(p), str(out)))
+    child_env = dict(os.environ)
+    child_env.update(kv.split("=", 1) for kv in env.split())
+    r = subprocess.run([sys.executable, "-c", code], env=child_env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert np.array_equal(np.load(out).reshape(img.shape), img), env
+
+
+@pytest.mark.parametrize("env", ["LFM_DECODE_CHUNK_BLOCKS=1", "LFM_DECODE_CHUNK_BLOCKS=1 LFM_DECODE_SLOTS=3",
+                                 "LFM_DECODE_CHUNK_BLOCKS=0", "LFM_DECODE_CHUNK_BLOCKS=1 LFM_DECODE_H2D=2"])
+def test_decode_chunk_pipeline(lfmlib, oracle, gpu, tmp_path, env):
+    """The pipelined GPU decode (chunks of whole block slabs on 2-3 HIP
+    streams, downloads on their own thread) restores the pixels whatever the
+    chunking: one slab per chunk on a video tiles stack of two t-volumes with
+    3-frame blocks puts chunk starts on odd (temporal) frames, whose previous
+    frame comes from the chunk before (event hand-over), and on volume starts;
+    one chunk; the hipMemcpyAsync upload.  Each variant runs in its own child
+    process (the switches are read once per process)."""
+    import subprocess
+    import sys
+    from conftest import PKG
+    img = oracle.synthetic_lf(200, 136, Z=10, C=1, Tn=2, T=13, seed=77)
+    lfmlib.set_family("tiles")
+    p = tmp_path / "ck.lfm"
+    lfmlib.write_lfm(str(p), img, predictor_request=8 + 4, nnum=13, video=1, block_size=[64, 64, 3, 1, 1])
+    out = tmp_path / "out.npy"
+    code = ("import sys; sys.path.insert(0, %r); import numpy as np, lfm; lfm.set_family('tiles'); "
             "o, _, _ = lfm.read_lfm(%r); np.save(%r, o)" % (PKG, str(p), str(out)))
     child_env = dict(os.environ)
     child_env.update(kv.split("=", 1) for kv in env.split())
