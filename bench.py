@@ -687,9 +687,13 @@ def main():
     alg_bytes = px_rank * 4  # 2 B read + 2 B written per pixel (no temporal frames in this config)
     achieved = alg_bytes / (pred_ms / 1e3) / 1e9
     traffic = None
-    tpath = os.path.join(REPO, "profiles", "r03_traffic_predict.json")
-    if not os.path.exists(tpath):
-        tpath = os.path.join(REPO, "profiles", "r02_traffic_predict.json")
+    # the newest PMC traffic file of the kernel (rocprofv3 --pmc FETCH_SIZE /
+    # WRITE_SIZE passes over scripts/encode_probe.py, scripts/pmc_summary.py)
+    tpath = None
+    for name in ("r04_traffic_predict.json", "r03_traffic_predict.json", "r02_traffic_predict.json"):
+        tpath = os.path.join(REPO, "profiles", name)
+        if os.path.exists(tpath):
+            break
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
