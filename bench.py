@@ -678,7 +678,7 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0)
     # one unpipelined encode (select + encode + every copy, nothing in flight), for its latency
     t1 = time.perf_counter()
-    enc.wait(enc.submit(d_img, z0, header_version=0, nnum=T, select_frame=sel_frame), copy=False)
+    _, lat_st = enc.wait(enc.submit(d_img, z0, header_version=0, nnum=T, select_frame=sel_frame), copy=False)
     latency_ms = max_over_ranks(time.perf_counter() - t1) * 1e3
 
     px_rank = X * Y * zf
@@ -724,7 +724,13 @@ def main():
                                "per lane, %d frames per launch)" % zf,
                      "traffic_file": os.path.relpath(tpath, REPO) if traffic is not None else None,
                      "kernel_ms": round(pred_ms, 4), "algorithmic_bytes": alg_bytes,
-                     "read_only_frac": round(px_rank * 2 / (pred_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
+                     "read_only_frac": round(px_rank * 2 / (pred_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                     # the timed region's launches share the CUs with the previous
+                     # encode's bzip2 tail (the next predictor stage starts before
+                     # that encode is released); the unpipelined latency encode's
+                     # launch has the GPU to itself
+                     "kernel_ms_alone": round(float(lat_st["predict_ms"]), 4),
+                     "frac_alone": round(alg_bytes / (float(lat_st["predict_ms"]) / 1e3) / 1e9 / PEAK_HBM_GBS, 4)},
         "stages_ms": {k: round(float(np.mean([s[k] for s in stats])), 3)
                       for k in ("select_ms", "predict_ms", "d2h_ms", "compress_ms", "total_ms")},
         "pipelined": "two encodes in flight (lfm_encoder_submit / wait): an encode's kernels overlap the previous "

@@ -556,7 +556,14 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     // a host stack starts its chunked upload (and the predictor on the chunks
     // that have landed) before the previous encode is released: the PCIe
     // upload runs under the previous encode's GPU bzip2
-    const bool host_early = gpu_bz && upload_pipe_ok(dev, h);
+    // a device stack, too, runs its selection and predictor stage before that
+    // wait, beside the previous encode's tail (its own buffer set; the
+    // selection then queues behind that tail, ~12 ms of host wall time, and the
+    // predictor kernel shares the CUs): config 3 pipelined 12 068-12 158 vs
+    // 11 797-11 872 Mpixel/s, same box (profiles/r04_ab_predict_early.txt);
+    // LFM_PREDICT_EARLY=0 waits for the release first
+    static const bool predict_early = env_int("LFM_PREDICT_EARLY", 1) == 1;
+    const bool host_early = gpu_bz && (upload_pipe_ok(dev, h) || (predict_early && dev));
     f.ticket = next_ticket_++;
     f.rc = 0;
     std::memset(&f.st, 0, sizeof(f.st));
