@@ -335,8 +335,9 @@ def config5_host_leg(local, threads, nvol):
     13, auto) in one host array -> lfm_encoder_encode_multi (the block
     scheduler behind klb_imageIO::writeImage; t-volumes farmed over the
     visible devices, chunked uploads overlapped with the predictor and GPU
-    bzip2) -> one in-memory .lfm; volumes 0..3 SHA-256-checked against the
-    oracle (cfg5x4), then the host input is released and every volume is
+    bzip2) -> one in-memory .lfm; volumes 0..3 and, when present, 50 and 99
+    SHA-256-checked against the oracle (cfg5x4, cfg5far: the far ones lie
+    past 2^32 in the offset table), then the host input is released and every volume is
     read back on its own (lfm_decode_memory_roi, readKLBroiInPlace's path)
     and compared with its regenerated pixels.  Peak RSS is the process's."""
     import resource
@@ -374,12 +375,29 @@ def config5_host_leg(local, threads, nvol):
         nb = 4 * 43 * 43  # blocks per volume (96 x 96 x 8)
         offs = np.frombuffer(b, dtype="<u8", count=nvol * nb, offset=320)
         base, prev, sha_ok = 320 + 8 * nvol * nb, 0, None
+        checked = []
         if e is not None:
             sha_ok = True
             for t in range(min(4, nvol)):
                 end = int(offs[(t + 1) * nb - 1])
                 sha_ok = sha_ok and hashlib.sha256(b[base + prev:base + end]).hexdigest() == e["volume_sha256"][t]
+                checked.append(t)
                 prev = end
+        # far volumes (t = 50, 99 of the 100-volume stack): streams at u64
+        # end-offsets past 2^32 against the oracle's per-volume digests
+        far = _manifest("cfg5far_4096x4096x32x1x100_video_tiles_auto")
+        far_max_offset = 0
+        if far is not None:
+            for ts, want in far["volumes"].items():
+                t = int(ts)
+                if t >= nvol:
+                    continue
+                a0 = int(offs[t * nb - 1]) if t else 0
+                a1 = int(offs[(t + 1) * nb - 1])
+                got = hashlib.sha256(b[base + a0:base + a1]).hexdigest() == want["sha256"] and a1 - a0 == want["bytes"]
+                sha_ok = (sha_ok is not False) and got
+                checked.append(t)
+                far_max_offset = max(far_max_offset, a1)
         lfm_bytes = len(b)
         del img
         exact, dec_s = True, 0.0
@@ -401,8 +419,9 @@ def config5_host_leg(local, threads, nvol):
     out.update({"volumes": nvol, "encode_Mpixel_per_s": round(px / enc_s / 1e6, 1), "encode_s": round(enc_s, 3),
                 "encode_first_call_s": round(enc_runs[0], 3),
                 "h2d_ms": round(st["h2d_ms"], 1), "ratio": round(px * 2 / lfm_bytes, 4),
-                "verified": {"against": "cfg5x4 per-volume SHA-256 of volumes 0..%d (oracle, reference bzip2-1.0.6)"
-                                        % (min(4, nvol) - 1), "ok": sha_ok},
+                "verified": {"against": "per-volume SHA-256 of volumes %s (cfg5x4 / cfg5far manifests: oracle, "
+                                        "reference bzip2-1.0.6)" % checked, "ok": sha_ok,
+                             "max_checked_end_offset": far_max_offset},
                 "decode_Mpixel_per_s": round(px / dec_s / 1e6, 1), "decode_s": round(dec_s, 3),
                 "decode_exact": exact,
                 "peak_rss_GB": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024 / 1e9, 2),

@@ -170,10 +170,12 @@ LFM_API void lfm_release_encoders(void);
 /* Decode an in-memory .lfm into `img` (host, getImageSizeBytes bytes). */
 LFM_API int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, int numThreads);
 /* Decode the region lb .. ub (inclusive, xyzct) of an in-memory .lfm into
- * `out` (host, x fastest, the region's size): readKLBroiInPlace on memory.
- * Only the blocks the region depends on are decoded. */
+ * `out` (host, x fastest, out_bytes long): readKLBroiInPlace on memory.
+ * Only the blocks the region depends on are decoded.  Returns 3 when the
+ * region lies outside the image or out_bytes is less than the region's
+ * pixels times the file's bytes per pixel (the header's data type). */
 LFM_API int lfm_decode_memory_roi(const uint8_t* buf, uint64_t len, const uint32_t lb[KLB_DATA_DIMS],
-                                  const uint32_t ub[KLB_DATA_DIMS], void* out, int numThreads);
+                                  const uint32_t ub[KLB_DATA_DIMS], void* out, uint64_t out_bytes, int numThreads);
 
 #ifdef __cplusplus
 }

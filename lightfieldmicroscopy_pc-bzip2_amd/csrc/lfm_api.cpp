@@ -253,12 +253,18 @@ extern "C" int lfm_decode_memory(const uint8_t* buf, uint64_t len, void* img, in
 }
 
 extern "C" int lfm_decode_memory_roi(const uint8_t* buf, uint64_t len, const uint32_t lb[KLB_DATA_DIMS],
-                                     const uint32_t ub[KLB_DATA_DIMS], void* out, int numThreads)
+                                     const uint32_t ub[KLB_DATA_DIMS], void* out, uint64_t out_bytes, int numThreads)
 {
     if (!buf || !lb || !ub || !out) return 3;
     klb_image_header h;
     int rc = h.parseHeader(buf, len);
     if (rc) return rc;
+    uint64_t need = h.getBytesPerPixel();  // the region in the file's own data type
+    for (int d = 0; d < KLB_DATA_DIMS; ++d) {
+        if (ub[d] < lb[d] || ub[d] >= h.xyzct[d]) return 3;
+        need *= (uint64_t)(ub[d] - lb[d] + 1);
+    }
+    if (!need || out_bytes < need) return 3;
     const size_t hs = h.getSizeInBytes();
     return lfm::decode_roi(buf + hs, len - hs, h, lb, ub, (uint8_t*)out, numThreads, lfm::current_family());
 }

@@ -122,7 +122,13 @@ struct Batch {
     uint32_t* out_bytes;
     uint32_t* wide;          // (stream, table) tasks whose heap weights exceed 17 bits
     uint32_t* wide_cnt;
-    uint32_t tie_direct;     // tie_runs_direct resolves short runs of equal prefixes from the text (LFM_TIE_DIRECT)
+    // two-stage BWT (bwt_bucket, bwt_induce)
+    uint32_t* nsub;          // rotations sorted per stream (the A or B rotations, or all of them)
+    uint32_t* bwt_mode;      // per stream: kModeSortA / kModeSortB / kModeFull
+    uint32_t* abcnt;         // per stream: A rotations per first byte [256], then B rotations [256]
+    uint32_t* sfin;          // the final order of every rotation (bwt_place_sorted / bwt_induce)
+    uint32_t* sfhi;          // bwt_induce's second entry word per position
+    uint32_t it_full;        // sort every rotation (no induction): the fallback for ties that need doubling
 };
 
 __device__ __forceinline__ uint32_t crc_feed(uint32_t c, uint32_t b) { return (c << 8) ^ c_crc_table[(c >> 24) ^ b]; }
@@ -599,35 +605,95 @@ __device__ __forceinline__ uint32_t bkt_slot(uint32_t key)
     return key ^ ((key >> (BITS - 8)) & 31u);
 }
 
+// Two-stage BWT (Itoh & Tanaka).  Rotation i is of type B when it sorts
+// before rotation i + 1 (T[i] < T[i + 1], or equal bytes and i + 1 of type B)
+// and of type A otherwise; the types of a non-periodic block are well defined
+// cyclically.  Only the rotations of ONE type (about half) go through the sort
+// below (bucket pass, chunk sorts, ties); bwt_induce places the others by one
+// scan of the sorted order.  Inside the bucket of first byte c the A rotations
+// come first; the A rotations of a bucket are ordered as their successors are
+// (i + 1 precedes i in the final order) and the B rotations likewise (i + 1
+// follows i).  So with the B rotations sorted a left-to-right scan places the
+// A ones (kModeSortB), with the A rotations sorted a right-to-left scan places
+// the B ones (kModeSortA).  The pass sorts the A rotations unless the B ones
+// are clearly fewer: on 16-bit little-endian symbols the A rotations start at
+// the low bytes, whose first byte spreads them over the buckets, while the B
+// ones start at the (mostly zero) high bytes.  rot_type reads tile[1 + k + d]
+// for d <= 8 (the tile holds 8 bytes past its end): 1 = B, 0 = A, 2 = still
+// undecided after 8 equal bytes (only runs of 0xFB survive RLE1 that long: the
+// stream is then sorted whole, kModeFull).
+constexpr uint32_t kModeSortA = 0, kModeSortB = 1, kModeFull = 2;
+
+__device__ __forceinline__ uint32_t rot_type(const uint8_t* tile, uint32_t k, uint32_t a, uint32_t b)
+{
+    if (a != b) return a < b ? 1u : 0u;
+#pragma unroll 1
+    for (uint32_t d = 1; d < 8; ++d) {
+        const uint32_t x = tile[1 + k + d], y = tile[2 + k + d];
+        if (x != y) return x < y ? 1u : 0u;
+    }
+    return 2u;
+}
+
+// does rotation k of the tile (first bytes a, b) go through the sort in `mode`
+__device__ __forceinline__ bool rot_sorted(const uint8_t* tile, uint32_t k, uint32_t a, uint32_t b, uint32_t mode)
+{
+    return mode == kModeFull || rot_type(tile, k, a, b) == (mode == kModeSortB ? 1u : 0u);
+}
+
 template <uint32_t BITS>
-__global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists L)
+__global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(8))) void bwt_bucket(Batch B, ChunkLists L)
 {
     constexpr uint32_t kBuckets = 1u << BITS;
-    __shared__ uint32_t hist[kBuckets];  // 128 KiB at 15 bits
+    __shared__ uint32_t hist[kBuckets];  // 64 KiB at 14 bits
     __shared__ uint8_t tile[kBktTile + 16];
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
     __shared__ uint32_t ccount[4], cbase[4];
-    __shared__ uint32_t sinuse[8];  // bytes present in the RLE1 text (the stream's inUse map)
+    __shared__ uint32_t sinuse[8];                  // bytes present in the RLE1 text (the stream's inUse map)
+    __shared__ uint32_t cnt_u[256], cnt_s[256];     // unsorted / sorted rotations per first byte
+    __shared__ uint32_t undecided, n_unsorted;
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
     const uint8_t* T = B.T + (size_t)s * B.cap;
     const uint32_t o = s * B.cap;
-    // the chunk sorts flag positions < n; tie_compact's 16-byte loads also
-    // see up to 15 bytes past n, which must read as "not tied"
-    if (t < 16 && n + t < B.cap) B.uflag[o + n + t] = 0;
-    for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
     if (t < 4) ccount[t] = 0;
     if (t < 8) sinuse[t] = 0;
-    // histogram of the BITS-bit bucket
-    BktPart nx = bucket_fetch(T, n, 0);
-    for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
-        const BktPart cur = nx;
-        nx = bucket_fetch(T, n, i0 + kBktTile);
-        const uint32_t m = bucket_put(cur, n, i0, tile);
-        for (uint32_t k = t; k < m; k += kBucketThreads)
-            atomicAdd(&hist[bkt_slot<BITS>(((uint32_t)tile[1 + k] << (BITS - 8)) | (tile[2 + k] >> (16 - BITS)))], 1u);
+    // histogram of the BITS-bit bucket over the rotations to sort; the pass
+    // restarts (at most twice) for the B rotations when they are clearly fewer
+    // and for every rotation when a type is undecided
+    uint32_t mode = B.it_full ? kModeFull : kModeSortA;
+    for (;;) {
+        for (uint32_t b = t; b < kBuckets; b += kBucketThreads) hist[b] = 0;
+        if (t < 256) cnt_u[t] = cnt_s[t] = 0;
+        if (t == 0) undecided = n_unsorted = 0;
+        __syncthreads();
+        BktPart nx = bucket_fetch(T, n, 0);
+        for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
+            const BktPart cur = nx;
+            nx = bucket_fetch(T, n, i0 + kBktTile);
+            const uint32_t m = bucket_put(cur, n, i0, tile);
+            for (uint32_t k = t; k < m; k += kBucketThreads) {
+                const uint32_t a = tile[1 + k], b = tile[2 + k];
+                const uint32_t ty = mode == kModeFull ? 3u : rot_type(tile, k, a, b);
+                if (ty == 2u) undecided = 1u;
+                else if (mode == kModeFull || ty == (mode == kModeSortB ? 1u : 0u))
+                    atomicAdd(&hist[bkt_slot<BITS>((a << (BITS - 8)) | (b >> (16 - BITS)))], 1u);
+                else atomicAdd(&cnt_u[a], 1u);
+            }
+            __syncthreads();
+        }
+        if (mode == kModeFull) break;
+        if (undecided) {
+            mode = kModeFull;
+        } else {
+            if (t < 256 && cnt_u[t]) atomicAdd(&n_unsorted, cnt_u[t]);
+            __syncthreads();
+            // the other type clearly fewer (by 1/8): sort it instead
+            if (mode != kModeSortA || (uint64_t)n_unsorted * 8 >= (uint64_t)(n - n_unsorted) * 7) break;
+            mode = kModeSortB;
+        }
         __syncthreads();
     }
     // exclusive scan of the buckets; chunk cuts at bucket ends
@@ -635,10 +701,7 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     static_assert(per <= (1u << (BITS - 8)), "a thread's buckets share their first byte");
     uint32_t sum = 0;
     for (uint32_t q = 0; q < per; ++q) sum += hist[bkt_slot<BITS>(t * per + q)];
-    if (sum) {  // every byte of the text starts a rotation: byte c is present iff its buckets are not empty
-        const uint32_t c = (t * per) >> (BITS - 8);
-        atomicOr(&sinuse[c >> 5], 1u << (c & 31));
-    }
+    if (sum) atomicAdd(&cnt_s[(t * per) >> (BITS - 8)], sum);
     uint32_t isum = sum;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t a = __shfl_up(isum, d);
@@ -646,9 +709,18 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     }
     if (lane == 63) wsum[wave] = isum;
     __syncthreads();
-    uint32_t psum = 0;
-    for (uint32_t w = 0; w < wave; ++w) psum += wsum[w];
+    uint32_t psum = 0, nsub = 0;
+    for (uint32_t w = 0; w < kBucketThreads / 64; ++w) {
+        if (w < wave) psum += wsum[w];
+        nsub += wsum[w];
+    }
     const uint32_t my0 = psum + isum - sum;
+    // every byte of the text starts a rotation: byte c is present iff it
+    // starts a sorted or an unsorted rotation
+    if (t < 256 && (cnt_u[t] | cnt_s[t])) atomicOr(&sinuse[t >> 5], 1u << (t & 31));
+    // the chunk sorts flag positions < nsub; tie_compact's 16-byte loads also
+    // see up to 15 bytes past nsub, which must read as "not tied"
+    if (t < 16 && nsub + t < B.cap) B.uflag[o + nsub + t] = 0;
     // cut positions of this thread's buckets (ascending): after a bucket that
     // holds a multiple of kChunk, and around a bucket larger than kChunk
     auto cuts_of = [&](auto&& emit) {
@@ -689,6 +761,14 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         });
     }
     if (t < 8) B.inuse[s * 8 + t] = sinuse[t];  // (written after the scan's barrier)
+    if (t < 256) {  // A / B rotations per first byte for bwt_induce
+        B.abcnt[(size_t)s * 512 + t] = mode == kModeSortA ? cnt_s[t] : cnt_u[t];
+        B.abcnt[(size_t)s * 512 + 256 + t] = mode == kModeSortA ? cnt_u[t] : cnt_s[t];
+    }
+    if (t == 0) {
+        B.nsub[s] = nsub;
+        B.bwt_mode[s] = mode;
+    }
     // bucket starts for the scatter
     {
         uint32_t off = my0;
@@ -699,12 +779,12 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
         }
     }
     __syncthreads();
-    // chunks = runs between consecutive cuts (the last ends at n)
+    // chunks = runs between consecutive cuts (the last ends at nsub)
     const uint32_t nch = min(tcut, kMaxCuts - 1) + 1;
     uint32_t cb = 0, ce = 0, cls = 0, slot = 0;
     if (t < nch) {
         cb = t ? cuts[t - 1] : 0u;
-        ce = t + 1 < nch ? cuts[t] : n;
+        ce = t + 1 < nch ? cuts[t] : nsub;
         const uint32_t m = ce > cb ? ce - cb : 0u;
         cls = m <= kTinyCap ? 3u : (m <= kSmallCap ? 0u : (m <= kBigCap ? 1u : 2u));
         if (m) slot = atomicAdd(&ccount[cls], 1u);
@@ -720,19 +800,23 @@ __global__ __launch_bounds__(kBucketThreads) void bwt_bucket(Batch B, ChunkLists
     // scatter of the values only (start | preceding byte << 24): the sorters
     // rebuild the 8-byte keys from the text (rot_key8_fast), which the L2s
     // hold, instead of 8-byte scattered key writes and their re-read
-    nx = bucket_fetch(T, n, 0);
+    BktPart nx = bucket_fetch(T, n, 0);
     for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
         const BktPart cur = nx;
         nx = bucket_fetch(T, n, i0 + kBktTile);
         const uint32_t m = bucket_put(cur, n, i0, tile);
         for (uint32_t k = t; k < m; k += kBucketThreads) {
             const uint8_t* p = tile + 1 + k;
-            const uint32_t pos = atomicAdd(&hist[bkt_slot<BITS>(((uint32_t)p[0] << (BITS - 8)) | (p[1] >> (16 - BITS)))], 1u);
-            B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
+            const uint32_t a = p[0], b = p[1];
+            if (rot_sorted(tile, k, a, b, mode)) {
+                const uint32_t pos = atomicAdd(&hist[bkt_slot<BITS>((a << (BITS - 8)) | (b >> (16 - BITS)))], 1u);
+                B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
+            }
         }
         __syncthreads();
     }
 }
+
 
 // the first-round key of rotation i of a stream's text T (length n): its
 // 8-byte prefix, big endian.  Away from the wrap, three aligned dwords (the
@@ -755,6 +839,22 @@ __device__ __forceinline__ uint64_t rot_key8_fast(const uint8_t* __restrict__ T,
         j = j + 1 == n ? 0u : j + 1;
     }
     return k;
+}
+
+// text_prev4: T[i-2] | T[i-3] << 8 | T[i-4] << 16 | T[i-5] << 24 (cyclic)
+__device__ __forceinline__ uint32_t text_prev4(const uint8_t* __restrict__ T, uint32_t n, uint32_t i)
+{
+    // two aligned dwords around T[i-5 .. i-2] (i - 1 < n: inside the text),
+    // loaded at a clamped address; the first five rotations wrap
+    const uint32_t a = i >= 5 ? i - 5 : 0u;
+    const uint32_t* w = (const uint32_t*)(T + (a & ~3u));
+    const uint64_t x = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    uint32_t r = __builtin_bswap32((uint32_t)(x >> ((a & 3u) * 8u)));
+    if (i < 5) {
+        r = 0;
+        for (uint32_t k = 2; k <= 5; ++k) r |= (uint32_t)T[(i + 5 * n - k) % n] << (8 * (k - 2));
+    }
+    return r;
 }
 
 // keys_a for the chunks the rocPRIM segmented sort takes (one workgroup per chunk)
@@ -943,361 +1043,6 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     }
 }
 
-// Hand-written chunk sort, LDS merge path (LFM_CS_ALGO=1; measured slower than
-// the rocPRIM kernel above: bz_bwt_ms 13.0 vs 11.0-11.5, same box).  Built to
-// issue fewer VALU instructions than rocPRIM's ~327 lane-ops per rotation; it
-// does (~300), but its blocked 16-byte LDS writes and random merge reads run
-// 8.6 bank-conflict cycles per LDS instruction against rocPRIM's 3.1
-// (profiles/r03_pmc_chunk_sorts.txt).
-//  - every lane owns IPT = 8 rotations (striped loads, keys rebuilt from the
-//    text), sorted in registers by Batcher's 19-exchange network;
-//  - merge levels L = 8 .. NI/2 through one LDS key / value array: each lane
-//    finds its 8 outputs' start on the merge path (log2 L + 1 probes) and
-//    merges them sequentially, tracking LDS indices only -- the values are
-//    gathered once per level by index, not selected at every step;
-//  - the levels whose pairs of runs lie inside one wave's 8 x 64 items need
-//    no s_barrier (one wave's LDS operations execute in order): only the last
-//    log2(TH / 64) levels synchronise the workgroup.
-// Padding slots (j >= m) sort as key ~0 with value kPad; a real rotation whose
-// 8-byte prefix is all ones (possible only in the chunk of the last bucket)
-// ties with them, so such a chunk compacts its real values below m afterwards.
-constexpr uint32_t kPad = 0xFFFFFFFFu;  // never a value: rotation starts are < 2^24
-
-__device__ __forceinline__ void wave_lds_order()
-{
-    // a compiler barrier between one wave's LDS writes and its later reads of
-    // other lanes' slots (the hardware executes a wave's DS instructions in order)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int I, int J>
-__device__ __forceinline__ void cs_exchange(uint64_t* k, uint32_t* v)
-{
-    const bool sw = k[I] > k[J];
-    const uint64_t a = k[I], b = k[J];
-    const uint32_t x = v[I], y = v[J];
-    k[I] = sw ? b : a;
-    k[J] = sw ? a : b;
-    v[I] = sw ? y : x;
-    v[J] = sw ? x : y;
-}
-
-template <int TH, int IPT>
-__global__ __launch_bounds__(TH) void bwt_chunk_msort(Batch B, const uint32_t* __restrict__ cbp,
-                                                      const uint32_t* __restrict__ cep, uint32_t nch, uint32_t per)
-{
-    static_assert(IPT == 8 && TH >= 64 && (TH & (TH - 1)) == 0, "8 items per lane, power-of-two workgroup");
-    constexpr uint32_t NI = TH * IPT;
-    constexpr uint32_t WI = 64 * IPT;  // one wave's items
-    __shared__ uint64_t sk[NI];
-    __shared__ uint32_t sv[NI];
-    __shared__ uint32_t s_nmax;
-    const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
-    if (c >= nch) return;
-    const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
-    const uint32_t s = cb / B.cap, n = B.n[s];
-    const uint8_t* T = B.T + (size_t)s * B.cap;
-    if (t == 0) s_nmax = 0;
-    uint64_t k[IPT];
-    uint32_t v[IPT];
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = q * TH + t;
-        v[q] = j < m ? B.vals_a[cb + j] : kPad;
-    }
-    uint32_t nmax = 0;
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const bool real = v[q] != kPad;
-        k[q] = real ? rot_key8_fast(T, n, v[q] & kIdxMask) : ~0ull;
-        nmax += (real && k[q] == ~0ull) ? 1u : 0u;
-    }
-    // Batcher's odd-even merge sort of 8
-    cs_exchange<0, 1>(k, v); cs_exchange<2, 3>(k, v); cs_exchange<4, 5>(k, v); cs_exchange<6, 7>(k, v);
-    cs_exchange<0, 2>(k, v); cs_exchange<1, 3>(k, v); cs_exchange<4, 6>(k, v); cs_exchange<5, 7>(k, v);
-    cs_exchange<1, 2>(k, v); cs_exchange<5, 6>(k, v);
-    cs_exchange<0, 4>(k, v); cs_exchange<1, 5>(k, v); cs_exchange<2, 6>(k, v); cs_exchange<3, 7>(k, v);
-    cs_exchange<2, 4>(k, v); cs_exchange<3, 5>(k, v);
-    cs_exchange<1, 2>(k, v); cs_exchange<3, 4>(k, v); cs_exchange<5, 6>(k, v);
-    const uint32_t e0 = t * IPT;
-#pragma unroll 1
-    for (uint32_t L = IPT; L < NI; L *= 2) {
-        // this lane's run goes back to LDS once the previous level's readers of
-        // those slots (its pair of runs: L items) are done
-        if (L > IPT) {
-            if (L <= WI) wave_lds_order();
-            else __syncthreads();
-        }
-#pragma unroll
-        for (int q = 0; q < IPT; q += 2) {
-            *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
-        }
-        *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
-        *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
-        if (2 * L <= WI) wave_lds_order();
-        else __syncthreads();
-        // merge path: outputs d .. d + IPT - 1 of the pair (runs A, B at pb)
-        const uint32_t pb = e0 & ~(2 * L - 1), d = e0 - pb;
-        const uint64_t* A = sk + pb;
-        const uint64_t* Bk = A + L;
-        uint32_t lo = d > L ? d - L : 0u, hi = d < L ? d : L;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (A[mid] <= Bk[d - 1 - mid]) lo = mid + 1;
-            else hi = mid;
-        }
-        uint32_t i = lo, j = d - lo;
-        uint64_t a = A[min(i, L - 1)], b = Bk[min(j, L - 1)];
-        uint32_t idx[IPT];
-#pragma unroll
-        for (int q = 0; q < IPT; ++q) {
-            const bool ta = i < L && (j >= L || a <= b);
-            k[q] = ta ? a : b;
-            idx[q] = ta ? pb + i : pb + L + j;
-            i += ta ? 1u : 0u;
-            j += ta ? 0u : 1u;
-            if (q + 1 < IPT) {
-                const uint64_t x = sk[ta ? pb + min(i, L - 1) : pb + L + min(j, L - 1)];
-                a = ta ? x : a;
-                b = ta ? b : x;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < IPT; ++q) v[q] = sv[idx[q]];
-    }
-    if (nmax) atomicAdd(&s_nmax, nmax);
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < IPT; q += 2) *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
-    *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
-    *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
-    __syncthreads();
-    const uint32_t cm = s_nmax;
-    if (cm && m < NI) {
-        // slots [m - cm, NI) all hold key ~0: move the cm real values below m
-        if (t == 0) {
-            uint32_t w = m - cm;
-            for (uint32_t q = m - cm; q < NI && w < m; ++q)
-                if (sv[q] != kPad) sv[w++] = sv[q];
-        }
-        __syncthreads();
-    }
-    uint32_t nt = 0;
-    for (uint32_t q = t; q < m; q += TH) {
-        const uint64_t x = sk[q];
-        const bool f = (q > 0 && sk[q - 1] == x) || (q + 1 < m && sk[q + 1] == x);
-        B.sa[cb + q] = sv[q];
-        B.uflag[cb + q] = f ? 1 : 0;
-        nt += f ? 1u : 0u;
-    }
-    if (__any(nt)) {
-        for (int dd = 32; dd > 0; dd >>= 1) nt += __shfl_xor(nt, dd);
-        if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[s], nt);
-    }
-}
-
-// Register bitonic chunk sort (LFM_CS_ALGO=2; measured slower still: bz_bwt_ms
-// 15.2, ~450 VALU lane-ops per rotation -- the first round is bound by LDS and
-// VALU together, and rocPRIM's merge sort balances the two best of the three).
-// Element e = t * 8 + q sits in
-// register q of lane t for the whole sort: exchanges at item distance 1, 2, 4
-// are in-lane, at 8 .. 256 cross-lane (DPP quad_perm for lane xor 1 / 2,
-// ds_swizzle for 4 / 8, v_permlane16/32_swap for 16 / 32: no LDS bank and no
-// dependent LDS chains), and only distances >= 512 (across waves) go through
-// LDS.  Oblivious: the same instruction stream for every chunk.
-template <int M>
-__device__ __forceinline__ uint32_t lane_xor(uint32_t x)
-{
-    if constexpr (M == 1) return __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    else if constexpr (M == 2) return __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
-    else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 10));  // xor M within 32 lanes
-}
-
-// both members of the pair (lane, lane ^ M) for M = 16 / 32: lo = the element
-// of the lane with bit M clear, hi = the other
-template <int M>
-__device__ __forceinline__ void lane_pair(uint32_t x, uint32_t& lo, uint32_t& hi)
-{
-    if constexpr (M == 16) {
-        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        lo = r[0];
-        hi = r[1];
-    } else {
-        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        lo = r[0];
-        hi = r[1];
-    }
-}
-
-template <int I, int J>
-__device__ __forceinline__ void cs_exchange_dir(uint64_t* k, uint32_t* v, bool desc)
-{
-    const bool sw = (k[I] > k[J]) != desc;  // equal keys may swap: both stay in the lane
-    const uint64_t a = k[I], b = k[J];
-    const uint32_t x = v[I], y = v[J];
-    k[I] = sw ? b : a;
-    k[J] = sw ? a : b;
-    v[I] = sw ? y : x;
-    v[J] = sw ? x : y;
-}
-
-template <int D>  // in-lane half-cleaner at item distance D (1, 2, 4)
-__device__ __forceinline__ void bs_inlane(uint64_t* k, uint32_t* v, bool desc)
-{
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-        if ((q & D) == 0) {
-            const int p = q | D;
-            const bool sw = (k[q] > k[p]) != desc;
-            const uint64_t a = k[q], b = k[p];
-            const uint32_t x = v[q], y = v[p];
-            k[q] = sw ? b : a;
-            k[p] = sw ? a : b;
-            v[q] = sw ? y : x;
-            v[p] = sw ? x : y;
-        }
-}
-
-template <int M>  // cross-lane half-cleaner with lane ^ M (M = 1 .. 32)
-__device__ __forceinline__ void bs_xlane(uint64_t* k, uint32_t* v, bool keep_min, bool lower)
-{
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const uint32_t klo = (uint32_t)k[q], khi = (uint32_t)(k[q] >> 32);
-        if constexpr (M <= 8) {
-            const uint64_t tk = ((uint64_t)lane_xor<M>(khi) << 32) | lane_xor<M>(klo);
-            const uint32_t tv = lane_xor<M>(v[q]);
-            // ties keep their own element on both sides (no duplicate)
-            const bool take = keep_min ? tk < k[q] : k[q] < tk;
-            k[q] = take ? tk : k[q];
-            v[q] = take ? tv : v[q];
-        } else {
-            uint32_t l0, h0, l1, h1, lv, hv;
-            lane_pair<M>(klo, l0, h0);
-            lane_pair<M>(khi, l1, h1);
-            lane_pair<M>(v[q], lv, hv);
-            const uint64_t lk = ((uint64_t)l1 << 32) | l0, hk = ((uint64_t)h1 << 32) | h0;
-            // the lower lane's element is lk; keep min(lk, hk) or max (ties: each its own)
-            const bool c = lk > hk;
-            const bool pick_hi = keep_min ? c : !c;
-            const bool same = lk == hk;
-            const bool hi_side = !lower;
-            const bool take_hi = same ? hi_side : pick_hi;
-            k[q] = take_hi ? hk : lk;
-            v[q] = take_hi ? hv : lv;
-        }
-    }
-}
-
-template <int TH, int LOGN, int K, int J>
-__device__ __forceinline__ void bs_stages(uint64_t* k, uint32_t* v, uint32_t t, uint64_t* sk, uint32_t* sv)
-{
-    if constexpr (K <= LOGN) {
-        const bool desc = K == LOGN ? false : ((t >> (K - 3)) & 1u) != 0;
-        if constexpr (J < 3) {
-            bs_inlane<1 << J>(k, v, desc);
-        } else if constexpr (J < 9) {
-            const bool lower = ((t >> (J - 3)) & 1u) == 0;
-            bs_xlane<1 << (J - 3)>(k, v, lower != desc, lower);
-        } else {
-            // across waves: through LDS (lane t ^ 2^(J-3), same register)
-            const uint32_t e0 = t * 8;
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < 8; q += 2) *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
-            *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
-            *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
-            __syncthreads();
-            const uint32_t p0 = e0 ^ (1u << J);
-            const bool lower = (e0 & (1u << J)) == 0;
-            const bool keep_min = lower != desc;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint64_t tk = sk[p0 + q];
-                const uint32_t tv = sv[p0 + q];
-                const bool take = keep_min ? tk < k[q] : k[q] < tk;
-                k[q] = take ? tk : k[q];
-                v[q] = take ? tv : v[q];
-            }
-        }
-        if constexpr (J > 0) bs_stages<TH, LOGN, K, J - 1>(k, v, t, sk, sv);
-        else bs_stages<TH, LOGN, K + 1, K>(k, v, t, sk, sv);
-    }
-}
-
-template <int TH>
-__global__ __launch_bounds__(TH) void bwt_chunk_bsort(Batch B, const uint32_t* __restrict__ cbp,
-                                                      const uint32_t* __restrict__ cep, uint32_t nch, uint32_t per)
-{
-    constexpr int IPT = 8;
-    constexpr uint32_t NI = TH * IPT;
-    constexpr int LOGN = TH == 128 ? 10 : TH == 256 ? 11 : 12;
-    static_assert((1u << LOGN) == NI, "power-of-two chunk capacity");
-    __shared__ uint64_t sk[NI];
-    __shared__ uint32_t sv[NI];
-    __shared__ uint32_t s_nmax;
-    const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
-    if (c >= nch) return;
-    const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
-    const uint32_t s = cb / B.cap, n = B.n[s];
-    const uint8_t* T = B.T + (size_t)s * B.cap;
-    if (t == 0) s_nmax = 0;
-    uint64_t k[IPT];
-    uint32_t v[IPT];
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = q * TH + t;
-        v[q] = j < m ? B.vals_a[cb + j] : kPad;
-    }
-    uint32_t nmax = 0;
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const bool real = v[q] != kPad;
-        k[q] = real ? rot_key8_fast(T, n, v[q] & kIdxMask) : ~0ull;
-        nmax += (real && k[q] == ~0ull) ? 1u : 0u;
-    }
-    // lane runs of 8, ascending in even lanes and descending in odd ones
-    const bool d3 = (t & 1u) != 0;
-    cs_exchange_dir<0, 1>(k, v, d3); cs_exchange_dir<2, 3>(k, v, d3); cs_exchange_dir<4, 5>(k, v, d3); cs_exchange_dir<6, 7>(k, v, d3);
-    cs_exchange_dir<0, 2>(k, v, d3); cs_exchange_dir<1, 3>(k, v, d3); cs_exchange_dir<4, 6>(k, v, d3); cs_exchange_dir<5, 7>(k, v, d3);
-    cs_exchange_dir<1, 2>(k, v, d3); cs_exchange_dir<5, 6>(k, v, d3);
-    cs_exchange_dir<0, 4>(k, v, d3); cs_exchange_dir<1, 5>(k, v, d3); cs_exchange_dir<2, 6>(k, v, d3); cs_exchange_dir<3, 7>(k, v, d3);
-    cs_exchange_dir<2, 4>(k, v, d3); cs_exchange_dir<3, 5>(k, v, d3);
-    cs_exchange_dir<1, 2>(k, v, d3); cs_exchange_dir<3, 4>(k, v, d3); cs_exchange_dir<5, 6>(k, v, d3);
-    bs_stages<TH, LOGN, 4, 3>(k, v, t, sk, sv);
-    if (nmax) atomicAdd(&s_nmax, nmax);
-    const uint32_t e0 = t * IPT;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < IPT; q += 2) *(ulonglong2*)&sk[e0 + q] = make_ulonglong2(k[q], k[q + 1]);
-    *(uint4*)&sv[e0] = make_uint4(v[0], v[1], v[2], v[3]);
-    *(uint4*)&sv[e0 + 4] = make_uint4(v[4], v[5], v[6], v[7]);
-    __syncthreads();
-    const uint32_t cm = s_nmax;
-    if (cm && m < NI) {
-        if (t == 0) {
-            uint32_t w = m - cm;
-            for (uint32_t q = m - cm; q < NI && w < m; ++q)
-                if (sv[q] != kPad) sv[w++] = sv[q];
-        }
-        __syncthreads();
-    }
-    uint32_t nt = 0;
-    for (uint32_t q = t; q < m; q += TH) {
-        const uint64_t x = sk[q];
-        const bool f = (q > 0 && sk[q - 1] == x) || (q + 1 < m && sk[q + 1] == x);
-        B.sa[cb + q] = sv[q];
-        B.uflag[cb + q] = f ? 1 : 0;
-        nt += f ? 1u : 0u;
-    }
-    if (__any(nt)) {
-        for (int dd = 32; dd > 0; dd >>= 1) nt += __shfl_xor(nt, dd);
-        if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[s], nt);
-    }
-}
-
 // the first-round key of rotation i of stream s: its 8-byte prefix, big endian
 __device__ __forceinline__ uint64_t rot_key8(const Batch& B, uint32_t s, uint32_t i)
 {
@@ -1370,7 +1115,7 @@ __global__ __launch_bounds__(256) void tie_compact(Batch B, uint32_t* __restrict
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t base = B.done[s];
     if (base == ~0u) return;
-    const uint32_t n = B.n[s], o = s * B.cap;
+    const uint32_t n = B.nsub[s], o = s * B.cap;
     if (t == 0) carry = base;
     __syncthreads();
     for (uint32_t j0 = 0; j0 < n; j0 += 256 * 16) {
@@ -1612,6 +1357,283 @@ __global__ __launch_bounds__(256) void bwt_flag_periodic(Batch B, const uint32_t
         atomicOr(&B.flags[cl[c] / B.cap], kFlagHost);
 }
 
+// ------------------------------------------------------------ induction --
+// bwt_place_sorted + bwt_induce: the final order from the sorted rotations.
+// In the final order (position q) bucket c (first byte c) holds its A
+// rotations, then its B rotations.  One type is sorted (sa); the other is
+// placed by one scan: kModeSortB scans left to right placing the A rotations,
+// kModeSortA scans right to left placing the B rotations.  In "scan order" v
+// (q, or n - 1 - q) with bytes mirrored the same way (x' = x, or 255 - x),
+// bucket u = c' starts with its placed part, and the rotation i met in bucket u
+// induces i - 1 when b' = T[i-1]' > u, or b' == u and i was placed itself;
+// i - 1 takes the next free slot of bucket b''s placed part (head[b']).
+//
+// Entries: lo = i | nprev << 20 | placed << 23 | T[i-1] << 24 (the sort
+// value's layout, bits 20-23 free since n < 2^20), hi = T[i-2] | T[i-3] << 8
+// | T[i-4] << 16 | T[i] << 24: nprev of the three bytes before T[i-1] are
+// valid (3 for a sorted rotation, one fewer per induction: a longer chain of
+// placed rotations reads the text), and T[i] is the rotation's bucket.
+// bwt_place_sorted writes the sorted entries to their final positions in
+// sfin / sfhi and kIndPend to every position still to place; bwt_induce then
+// reads nothing else, and overwrites every position with its sort value.
+constexpr uint32_t kIndPend = 0xFFFFFFFFu;  // never an entry: nprev <= 3
+constexpr uint32_t kIndIdx = 0xFFFFFu;      // n < nblock_max < 2^20
+constexpr uint32_t kIndPlaced = 1u << 23;
+constexpr int kPlaceUnroll = 8;  // sorted slots per thread in flight (bwt_place_sorted)
+
+// q-order starts of each bucket (q0[c]), its placed part (p0[c], p1[c]) and
+// the first sa slot of its sorted rotations (s0[c]), 256 threads
+__device__ __forceinline__ void ind_tables(const Batch& B, uint32_t s, uint32_t mode, uint32_t* q0, uint32_t* p0,
+                                           uint32_t* p1, uint32_t* s0, uint32_t* wtmp)
+{
+    const uint32_t c = threadIdx.x, lane = c & 63, wave = c >> 6;
+    const uint32_t na = B.abcnt[(size_t)s * 512 + c], nb = B.abcnt[(size_t)s * 512 + 256 + c];
+    const uint32_t ns = mode == kModeSortA ? na : nb;  // sorted (kModeFull: all in the B counts)
+    uint32_t x = na + nb, y = ns;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a = __shfl_up(x, d), b = __shfl_up(y, d);
+        if ((int)lane >= d) {
+            x += a;
+            y += b;
+        }
+    }
+    if (lane == 63) {
+        wtmp[wave] = x;
+        wtmp[4 + wave] = y;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < wave; ++w) {
+        x += wtmp[w];
+        y += wtmp[4 + w];
+    }
+    const uint32_t qs = x - na - nb;
+    q0[c] = qs;
+    s0[c] = y - ns;
+    // placed part: the A rotations (kModeSortB), the B ones (kModeSortA), none (kModeFull)
+    p0[c] = mode == kModeSortA ? qs + na : qs;
+    p1[c] = mode == kModeSortA ? qs + na + nb : (mode == kModeSortB ? qs + na : qs);
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void bwt_place_sorted(Batch B)
+{
+    __shared__ uint32_t q0[256], p0[256], p1[256], s0[256], wtmp[8];
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s], ns = B.nsub[s], mode = B.bwt_mode[s];
+    if (n == 0) return;
+    ind_tables(B, s, mode, q0, p0, p1, s0, wtmp);
+    const size_t o = (size_t)s * B.cap;
+    const uint8_t* T = B.T + o;
+    uint32_t* SF = B.sfin + o;
+    uint32_t* SH = B.sfhi + o;
+    // the sorted slots, kPlaceUnroll per thread in flight: sa, then T[i-4 .. i]
+    constexpr int K = kPlaceUnroll;
+    for (uint32_t j0 = 0; j0 < ns; j0 += K * 256) {
+        uint32_t v[K], w0[K], w1[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = B.sa[o + min(j0 + k * 256 + t, ns - 1)];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {  // two aligned dwords (clamped; the first four rotations wrap)
+            const uint32_t i = v[k] & kIdxMask, a = i >= 4 ? i - 4 : 0u;
+            const uint32_t* w = (const uint32_t*)(T + (a & ~3u));
+            w0[k] = w[0];
+            w1[k] = w[1];
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t j = j0 + k * 256 + t;
+            if (j >= ns) break;
+            const uint32_t i = v[k] & kIdxMask;
+            uint32_t x;  // T[i-4] | T[i-3] << 8 | T[i-2] << 16 | T[i-1] << 24
+            uint32_t c;  // T[i]
+            if (i >= 4) {
+                const uint32_t sh = ((i - 4) & 3u) * 8u;
+                const uint64_t d = (uint64_t)w0[k] | ((uint64_t)w1[k] << 32);
+                x = (uint32_t)(d >> sh);
+                c = (uint32_t)(d >> (sh + 32)) & 0xFFu;
+            } else {
+                x = 0;
+                for (uint32_t q = 1; q <= 4; ++q) x |= (uint32_t)T[(i + 4 * n - q) % n] << (32 - 8 * q);
+                c = T[i];
+            }
+            const uint32_t q = (mode == kModeSortA ? q0[c] : p1[c]) + (j - s0[c]);
+            SF[q] = mode == kModeFull ? v[k] : (v[k] | (3u << 20));
+            SH[q] = ((x >> 16) & 0xFFu) | (((x >> 8) & 0xFFu) << 8) | ((x & 0xFFu) << 16) | (c << 24);
+        }
+    }
+    // the positions still to place
+    for (uint32_t c = 0; c < 256; ++c)
+        for (uint32_t q = p0[c] + t; q < p1[c]; q += 256) SF[q] = kIndPend;
+}
+
+// bwt_induce: one wave per stream scans in scan order, in blocks of
+// kIndSlices slices of 64 positions through an LDS ring of two blocks:
+// entries placed into the current or the next block go to the ring, those
+// further ahead to sfin / sfhi; while a block is scanned the next block's
+// entries are loaded (coalesced) and written into the ring after the scan
+// (kIndPend = not placed yet).  The inducing lanes of a slice are ranked per
+// b' with one ballot per distinct b' (the predecessors of a run of sorted
+// rotations take few distinct bytes), so the slots follow the scan order; an
+// entry still pending when its slice is scanned is placed by an earlier lane
+// of the same slice: the slice then runs in rounds up to its first pending lane.
+constexpr uint32_t kIndSlices = 8;
+constexpr uint32_t kIndBlock = 64 * kIndSlices;
+constexpr uint32_t kIndRing = 2 * kIndBlock;
+
+// LDS-DMA of one dword per lane into LDS at `lds` + 4 * lane, from L2 (sc1:
+// the entries were written by this wave earlier).  Inline asm: the compiler
+// does not track the DMA, so nothing of it ties up VGPRs while the wave works
+// (bwt_induce waits with vm_drain before it reads the staged entries).
+__device__ __forceinline__ void glds4(const uint32_t* g, const void* lds)
+{
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1" ::"s"(m0), "v"(g) : "memory", "m0");
+}
+
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__global__ __launch_bounds__(64) void bwt_induce(Batch B)
+{
+    __shared__ uint32_t head[256];  // next free scan position of bucket u's placed part
+    __shared__ uint2 ring[kIndRing];
+    __shared__ uint32_t stg[2][kIndBlock];  // the next block's entries as loaded (lo, hi)
+    const uint32_t s = blockIdx.x, lane = threadIdx.x;
+    if (B.flags[s] & kFlagHost) return;
+    const uint32_t n = B.n[s];
+    const uint32_t mode = B.bwt_mode[s];
+    if (n == 0 || mode == kModeFull) return;  // kModeFull: bwt_place_sorted wrote the final order
+    const bool rev = mode == kModeSortA;      // right to left, mirrored bytes
+    const uint32_t mir = rev ? 255u : 0u;
+    const size_t o = (size_t)s * B.cap;
+    uint32_t* SF = B.sfin + o;
+    uint32_t* SH = B.sfhi + o;
+    const uint8_t* T = B.T + o;
+    {  // head[u] = scan-order start of bucket u (its placed part comes first)
+        uint32_t nt[4], l = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t c = (4 * lane + q) ^ mir;
+            nt[q] = B.abcnt[(size_t)s * 512 + c] + B.abcnt[(size_t)s * 512 + 256 + c];
+            l += nt[q];
+        }
+        uint32_t x = l;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if ((int)lane >= d) x += y;
+        }
+        x -= l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            head[4 * lane + q] = x;
+            x += nt[q];
+        }
+    }
+    for (uint32_t i = lane; i < kIndRing; i += 64) ring[i].x = kIndPend;
+    // position in sfin of scan position v
+    const uint32_t qa = rev ? n - 1 : 0u;
+    auto qof = [&](uint32_t v) { return rev ? qa - v : v; };
+    auto issue = [&](uint32_t vb) {  // the block at vb into stg by LDS-DMA (clamped: every lane loads)
+#pragma unroll
+        for (uint32_t k = 0; k < kIndSlices; ++k) {
+            const uint32_t q = qof(min(vb + 64 * k + lane, n - 1));
+            glds4(SF + q, &stg[0][64 * k]);
+            glds4(SH + q, &stg[1][64 * k]);
+        }
+    };
+    auto stage = [&](uint32_t vb) {  // into the ring: entries known when loaded
+        vm_drain();
+#pragma unroll
+        for (uint32_t k = 0; k < kIndSlices; ++k) {
+            const uint32_t v = vb + 64 * k + lane;
+            const uint32_t lo = stg[0][64 * k + lane], hi = stg[1][64 * k + lane];
+            if (v < n && lo != kIndPend) ring[v % kIndRing] = make_uint2(lo, hi);
+        }
+    };
+    __syncthreads();
+    issue(0);
+    stage(0);
+    bool bad = false;  // inconsistent counts or a pending entry no earlier lane places (never)
+    for (uint32_t v0 = 0; v0 < n && !bad; v0 += kIndBlock) {
+        // the next block's ring slots held the previous block: not placed yet
+#pragma unroll
+        for (uint32_t k = 0; k < kIndSlices; ++k) ring[(v0 + kIndBlock + 64 * k + lane) % kIndRing].x = kIndPend;
+        const bool more = v0 + kIndBlock < n;
+        if (more) issue(v0 + kIndBlock);
+#pragma unroll
+        for (uint32_t k = 0; k < kIndSlices; ++k) {
+            const uint32_t v = v0 + 64 * k + lane;
+            const bool valid = v < n;
+            uint64_t todo = __ballot(valid);
+            if (!todo) break;
+            const uint32_t r = v % kIndRing;
+            uint2 e = ring[r];
+            uint64_t pend = __ballot(valid && e.x == kIndPend);
+            // rounds over the lanes before the first pending one (one round
+            // unless an entry of the slice is placed by an earlier lane)
+            for (;;) {
+                const uint64_t act = pend ? todo & ((pend & (0ull - pend)) - 1ull) : todo;
+                if (!act) {
+                    bad = true;
+                    break;
+                }
+                const bool me = (act >> lane) & 1u;
+                const uint32_t lo = e.x, hi = e.y;
+                const uint32_t b = (lo >> 24) ^ mir, u = (hi >> 24) ^ mir;
+                const bool ind = me && (b > u || (b == u && (lo & kIndPlaced)));
+                if (me) SF[qof(v)] = lo & ~(0xFu << 20);
+                uint64_t rem = __ballot(ind);
+                if (rem) {
+                    // rank among the inducing lanes with the same b: a ballot per distinct b
+                    uint32_t rank = 0, cnt = 0;
+                    do {
+                        const uint32_t bl = __builtin_amdgcn_readlane(b, __builtin_ctzll(rem));
+                        const uint64_t m = __ballot(b == bl) & rem;
+                        if ((m >> lane) & 1u) {
+                            rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            cnt = __popcll(m);
+                        }
+                        rem &= ~m;
+                    } while (rem);
+                    const uint32_t idx = lo & kIndIdx, np = (lo >> 20) & 7u;
+                    const uint32_t p = idx ? idx - 1 : n - 1;
+                    // entry of i - 1: T[p-1] = T[i-2] ... and T[p] = T[i-1]
+                    uint32_t plo = p | ((np - 1) << 20) | kIndPlaced | ((hi & 0xFFu) << 24);
+                    uint32_t phi = ((hi >> 8) & 0xFFFFu) | (lo & 0xFF000000u);
+                    if (ind && np == 0) {  // a chain of placed rotations longer than the carried bytes
+                        const uint32_t x = text_prev4(T, n, p + 1);  // T[p-1] .. T[p-4]
+                        plo = p | (3u << 20) | kIndPlaced | ((x & 0xFFu) << 24);
+                        phi = ((x >> 8) & 0xFFFFFFu) | (lo & 0xFF000000u);
+                    }
+                    uint32_t dest = 0;
+                    if (ind) dest = head[b] + rank;
+                    if (ind && rank == 0) head[b] = dest + cnt;
+                    if (__any(ind && dest >= n)) {
+                        bad = true;
+                        break;
+                    }
+                    if (ind) {
+                        if (dest < v0 + kIndRing) {
+                            ring[dest % kIndRing] = make_uint2(plo, phi);
+                        } else {
+                            SF[qof(dest)] = plo;
+                            SH[qof(dest)] = phi;
+                        }
+                    }
+                }
+                todo &= ~act;
+                if (!todo) break;
+                e = ring[r];
+                pend = __ballot(valid && e.x == kIndPend) & todo;
+            }
+            if (bad) break;
+        }
+        if (more && !bad) stage(v0 + kIndBlock);
+    }
+    if (bad && lane == 0) B.flags[s] |= kFlagHost;  // the host library redoes the stream
+}
+
 // ------------------------------------------------------------------ MTF --
 // compress.c generateMTFValues in three parallel steps.  The move-to-front
 // list in front of position j is a function of the last occurrences before
@@ -1714,125 +1736,6 @@ __global__ __launch_bounds__(256) void mtf_prefix(Batch B, uint32_t nseg_max, in
         const int32_t v = *p;
         *p = lb;
         lb = max(lb, v);
-    }
-}
-
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-// v_writelane_b32: lane `ln` of v takes the scalar x (both wave-uniform)
-__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t ln)
-{
-    const uint32_t xs = __builtin_amdgcn_readfirstlane(x);
-    const uint32_t ls = __builtin_amdgcn_readfirstlane(ln);
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(xs), "s"(ls) : "m0");
-    return v;
-}
-
-// pos += (pos < m) on two 16-bit positions per word: sat(m - pos) is
-// non-zero exactly below m, min(., 1) turns it into the increment
-__device__ __forceinline__ uint32_t inc_below(uint32_t w, uint32_t m2)
-{
-    uint32_t d, r;
-    asm volatile("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(d) : "s"(m2), "v"(w));
-    asm volatile("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(d) : "v"(d));
-    asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(w), "v"(d));
-    return r;
-}
-
-// The list is kept as its inverse: pos[c] = place of symbol c.  Lane l holds
-// pos of symbols 4l .. 4l+3 as 16-bit fields (w0: 4l, 4l+1; w1: 4l+2, 4l+3).
-// A step reads pos[ll] (the MTF value m) with one readlane, then every symbol
-// in front of it moves back one place (two packed adds per lane) and ll goes
-// to place 0 (one writelane); m == 0 (43 % of the steps) costs nothing.
-__global__ __launch_bounds__(256) void mtf_seg(Batch B, uint32_t nseg_max, const int32_t* __restrict__ seg_last)
-{
-    __shared__ int32_t key[4][256];
-    __shared__ uint32_t posw[4][128];  // 256 16-bit positions per wave
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t s = blockIdx.y, k = blockIdx.x * 4 + wave;
-    if (B.flags[s] & kFlagHost) return;
-    const uint32_t n = B.n[s];
-    const uint32_t j0 = k * kSeg;
-    if (j0 >= n) return;
-    const size_t o = (size_t)s * B.cap;
-    uint32_t nin = 0;
-    for (int q = 0; q < 8; ++q) nin += __popc(B.inuse[s * 8 + q]);
-    // list order at j0: seen symbols by last position (descending), then the
-    // unseen ones by symbol index (ascending) -- key(unseen c) = -1 - c
-    const int32_t* lb = seg_last + ((size_t)s * nseg_max + k) * 256;
-    uint16_t* pos = (uint16_t*)posw[wave];
-    for (uint32_t c = lane; c < 256; c += 64) {
-        const int32_t v = c < nin ? lb[c] : INT32_MIN;
-        key[wave][c] = (c < nin && v < 0) ? -1 - (int32_t)c : v;
-        pos[c] = 0xFFFFu;  // symbols not in use: never below any m
-    }
-    __builtin_amdgcn_wave_barrier();
-    __shared__ uint32_t front_sym[4];
-    for (uint32_t c = lane; c < nin; c += 64) {
-        const int32_t kc = key[wave][c];
-        uint32_t r = 0;
-        for (uint32_t d = 0; d < nin; ++d) r += key[wave][d] > kc ? 1u : 0u;
-        pos[c] = (uint16_t)r;
-        if (r == 0) front_sym[wave] = c;
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint32_t w0 = posw[wave][2 * lane], w1 = posw[wave][2 * lane + 1];
-    // the symbol at place 0, kept in a scalar: a repeat (m == 0, 43 % of the
-    // steps) costs one compare
-    uint32_t front = __builtin_amdgcn_readfirstlane(front_sym[wave]);
-    const uint8_t* llbuf = (const uint8_t*)B.mtfv + o;
-    uint8_t* mraw = B.uflag + o;
-    const uint32_t j1 = min(n, j0 + kSeg);
-    for (uint32_t jb = j0; jb < j1; jb += 256) {
-        // 256 symbols per round: lane l holds ll[jb + 4l .. jb + 4l + 3]
-        uint32_t llw = 0;
-        const uint32_t jl = jb + lane * 4;
-        if (jl + 3 < j1) {
-            llw = *(const uint32_t*)(llbuf + jl);  // 4-byte aligned: jb and o are multiples of 256
-        } else {
-            for (uint32_t q = 0; q < 4; ++q)
-                if (jl + q < j1) llw |= (uint32_t)llbuf[jl + q] << (8 * q);
-        }
-        const uint32_t ngrp = (min(256u, j1 - jb) + 3) >> 2;
-        uint32_t outw = 0;
-        for (uint32_t g = 0; g < ngrp; ++g) {
-            const uint32_t four = __builtin_amdgcn_readlane(llw, g);
-            uint32_t sout = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                const uint32_t c = __builtin_amdgcn_readfirstlane((four >> (8 * q)) & 0xFFu);
-                front = __builtin_amdgcn_readfirstlane(front);
-                if (c != front) {  // m = 0 otherwise: a uniform scalar branch
-                    front = c;
-                    // branch-free update: both words of lane c >> 2 are read,
-                    // both VGPRs take the increment, the word holding c is
-                    // replaced by a lane-select
-                    const uint32_t ln = c >> 2, hi = c & 1u, sel = (c >> 1) & 1u;
-                    const uint32_t a = __builtin_amdgcn_readlane(w0, ln), b = __builtin_amdgcn_readlane(w1, ln);
-                    const uint32_t word = sel ? b : a;
-                    const uint32_t m = (word >> (16 * hi)) & 0xFFFFu;
-                    uint32_t other = (word >> (16 - 16 * hi)) & 0xFFFFu;
-                    other += other < m ? 1u : 0u;
-                    const uint32_t nw = other << (16 - 16 * hi);
-                    const uint32_t m2 = m | (m << 16);
-                    w0 = inc_below(w0, m2);
-                    w1 = inc_below(w1, m2);
-                    const uint32_t l0 = sel ? 64u : ln, l1 = sel ? ln : 64u;
-                    w0 = lane == l0 ? nw : w0;
-                    w1 = lane == l1 ? nw : w1;
-                    sout |= (m & 0xFFu) << (8 * q);
-                }
-            }
-            outw = writelane(outw, sout, g);
-        }
-        if (jl < j1) {
-            if (jl + 3 < j1) {
-                *(uint32_t*)(mraw + jl) = outw;
-            } else {
-                for (uint32_t q = 0; q < 4; ++q)
-                    if (jl + q < j1) mraw[jl + q] = (uint8_t)(outw >> (8 * q));
-            }
-        }
     }
 }
 
@@ -2253,60 +2156,6 @@ __global__ __launch_bounds__(64) void huff_init(Batch B)
     }
 }
 
-// One workgroup per stream.  The MTF symbols are staged through LDS a tile
-// of kHuffThreads selector groups at a time (coalesced 16-byte loads); each
-// thread then costs one group from LDS and adds its symbols to the chosen
-// table's frequencies.
-constexpr uint32_t kSelTileSyms = kHuffThreads * kGSize;  // 12 800 symbols (25 KiB)
-
-__global__ __launch_bounds__(kHuffThreads) void huff_select(Batch B)
-{
-    __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
-    __shared__ uint64_t lpack[kMaxAlpha];  // the tables' lengths of a symbol, 10 bits each
-    __shared__ uint4 tbuf4[kSelTileSyms * 2 / 16];
-    const uint16_t* tbuf = (const uint16_t*)tbuf4;
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
-    if (B.flags[s] & kFlagHost) return;
-    const uint32_t nMTF = B.nmtf[s], nSel = B.nsel[s];
-    const int nGroups = (int)B.ngroups[s];
-    const int alphaSize = (int)stream_nin(B, s) + 2;
-    const uint8_t* len = B.len + (size_t)s * kMaxGroups * kMaxAlpha;
-    const uint16_t* mtfv = B.mtfv + (size_t)s * (B.cap + 8);  // 16-byte aligned rows
-    uint8_t* sel = B.sel + (size_t)s * B.sel_cap;
-    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rfreq[i / kMaxAlpha][i % kMaxAlpha] = 0;
-    for (int v = t; v < alphaSize; v += kHuffThreads) {
-        uint64_t lp = 0;
-        for (int q = 0; q < nGroups; ++q) lp |= (uint64_t)len[q * kMaxAlpha + v] << (10 * q);
-        lpack[v] = lp;
-    }
-    for (uint32_t g0 = 0; g0 < nSel; g0 += kHuffThreads) {
-        const uint32_t i0 = g0 * kGSize, i1 = min(nMTF, i0 + kSelTileSyms);
-        const uint32_t nv = (i1 - i0 + 7) / 8;  // 16-byte vectors (the row has 8 symbols of slack)
-        __syncthreads();
-        for (uint32_t v = t; v < nv; v += kHuffThreads) tbuf4[v] = *(const uint4*)(mtfv + i0 + 8 * v);
-        __syncthreads();
-        const uint32_t g = g0 + t;
-        if (g < nSel) {
-            const uint32_t gs = g * kGSize - i0, ge = min(nMTF, (g + 1) * kGSize) - i0;
-            // a group's cost under every table at once: 50 symbols x length <= 17
-            // stays below 1024 per 10-bit field (bzip2 sums UInt16 costs)
-            uint64_t acc = 0;
-            for (uint32_t i = gs; i < ge; ++i) acc += lpack[tbuf[i]];
-            int bt = -1;
-            uint32_t bc = 999999999u;
-            for (int q = 0; q < nGroups; ++q) {
-                const uint32_t cq = (uint32_t)(acc >> (10 * q)) & 1023u;
-                if (cq < bc) { bc = cq; bt = q; }
-            }
-            sel[g] = (uint8_t)bt;
-            for (uint32_t i = gs; i < ge; ++i) atomicAdd(&rfreq[bt][tbuf[i]], 1u);
-        }
-    }
-    __syncthreads();
-    uint32_t* rf = B.rfreq + (size_t)s * kMaxGroups * kMaxAlpha;
-    for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rf[i] = rfreq[i / kMaxAlpha][i % kMaxAlpha];
-}
-
 // huff_select with a group's 50 symbols loaded straight into registers (25
 // dword loads from its 100 bytes; a row is 16-byte aligned and 100 is a
 // multiple of 4): no LDS tile, so ~8 KiB of LDS per workgroup and more
@@ -2369,116 +2218,6 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
     __syncthreads();
     uint32_t* rf = B.rfreq + (size_t)s * kMaxGroups * kMaxAlpha;
     for (int i = t; i < kMaxGroups * kMaxAlpha; i += kHuffThreads) rf[i] = rfreq[i / kMaxAlpha][i % kMaxAlpha];
-}
-
-// BZ2_hbMakeCodeLengths for kLenTasks (stream, table) pairs per wave, one per
-// lane: the sequential heap code runs SIMT across tables instead of on one
-// lane.  Per-lane arrays are interleaved in LDS (element e of lane l at
-// e * kLenTasks + l: conflict-free): heap nodes and parents as u16, heap
-// weights as u32 (124 KiB for 48 lanes).  Leaf weights are recomputed from the
-// frequencies after a too-long retry (weight = 1 + weight / 2, per retry).
-constexpr int kLenTasks = 16;  // default lanes per wave (LFM_HUFF_LANES overrides: 1, 2, 4, 8, 16)
-
-
-// (LFM_HUFF_PACK=0; huff_lengths_heap below is the default)
-template <int kLenTasks>
-__global__ __launch_bounds__(64) void huff_lengths(Batch B)
-{
-    __shared__ uint16_t heap_n[(kMaxAlpha + 2) * kLenTasks];
-    __shared__ uint16_t par[(2 * kMaxAlpha) * kLenTasks];
-    __shared__ uint32_t heap_w[(kMaxAlpha + 2) * kLenTasks];
-    const uint32_t lane = threadIdx.x;
-    if (lane >= (uint32_t)kLenTasks) return;
-    auto run = [&](uint32_t task) {
-    const uint32_t s = task / kMaxGroups, tb = task % kMaxGroups;
-    if (s >= B.nstreams || (B.flags[s] & kFlagHost) || tb >= B.ngroups[s]) return;
-    const int alphaSize = (int)stream_nin(B, s) + 2;
-    const uint32_t* freq = B.rfreq + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
-    uint8_t* len = B.len + ((size_t)s * kMaxGroups + tb) * kMaxAlpha;
-#define HN(e) heap_n[(e) * kLenTasks + lane]
-#define HW(e) heap_w[(e) * kLenTasks + lane]
-#define PA(e) par[(e) * kLenTasks + lane]
-    int retries = 0;
-    while (true) {
-        int nNodes = alphaSize, nHeap = 0;
-        HN(0) = 0;
-        HW(0) = 0;
-        auto upheap = [&](int z) {
-            int zz = z;
-            const uint32_t tmp = HN(zz), tw = HW(zz);
-            while (tw < HW(zz >> 1)) {
-                HN(zz) = HN(zz >> 1);
-                HW(zz) = HW(zz >> 1);
-                zz >>= 1;
-            }
-            HN(zz) = (uint16_t)tmp;
-            HW(zz) = tw;
-        };
-        auto downheap = [&](int z) {
-            int zz = z;
-            const uint32_t tmp = HN(zz), tw = HW(zz);
-            while (true) {
-                int yy = zz << 1;
-                if (yy > nHeap) break;
-                if (yy < nHeap && HW(yy + 1) < HW(yy)) ++yy;
-                if (tw < HW(yy)) break;
-                HN(zz) = HN(yy);
-                HW(zz) = HW(yy);
-                zz = yy;
-            }
-            HN(zz) = (uint16_t)tmp;
-            HW(zz) = tw;
-        };
-        for (int i = 1; i <= alphaSize; ++i) {
-            uint32_t w = freq[i - 1] == 0 ? 1u : freq[i - 1];
-            for (int r = 0; r < retries; ++r) w = 1 + w / 2;
-            PA(i) = 0xFFFF;  // -1: no parent yet
-            ++nHeap;
-            HN(nHeap) = (uint16_t)i;
-            HW(nHeap) = w << 8;
-            upheap(nHeap);
-        }
-        while (nHeap > 1) {
-            const uint32_t n1 = HN(1), w1 = HW(1);
-            HN(1) = HN(nHeap);
-            HW(1) = HW(nHeap);
-            --nHeap;
-            downheap(1);
-            const uint32_t n2 = HN(1), w2 = HW(1);
-            HN(1) = HN(nHeap);
-            HW(1) = HW(nHeap);
-            --nHeap;
-            downheap(1);
-            ++nNodes;
-            PA(n1) = (uint16_t)nNodes;
-            PA(n2) = (uint16_t)nNodes;
-            const uint32_t d1 = w1 & 0xffu, d2 = w2 & 0xffu;
-            const uint32_t wn = ((w1 & 0xffffff00u) + (w2 & 0xffffff00u)) | (1u + (d1 > d2 ? d1 : d2));
-            PA(nNodes) = 0xFFFF;
-            ++nHeap;
-            HN(nHeap) = (uint16_t)nNodes;
-            HW(nHeap) = wn;
-            upheap(nHeap);
-        }
-        // depths top-down (a parent is created after its children)
-        for (int k = nNodes; k >= 1; --k) {
-            const uint32_t pk = PA(k);
-            PA(k) = (uint16_t)(pk == 0xFFFF ? 0 : PA(pk) + 1);
-        }
-        bool tooLong = false;
-        for (int i = 1; i <= alphaSize; ++i) {
-            const uint32_t j = PA(i);
-            len[i - 1] = (uint8_t)j;
-            if (j > 17) tooLong = true;
-        }
-        if (!tooLong) break;
-        ++retries;
-    }
-    };
-    run(blockIdx.x * kLenTasks + lane);
-#undef HN
-#undef HW
-#undef PA
 }
 
 // BZ2_hbMakeCodeLengths, kL (stream, table) heaps per wave, one per lane,
@@ -3244,7 +2983,7 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * align_up(raw_cap, 16), 256);   // raw
     b += align_up(N, 256);                                      // T
     b += 2 * align_up(N * 8, 256);                              // keys
-    b += 6 * align_up(N * 4, 256);                              // vals_a, sa, rank, vals_b, cl0, cl1
+    b += 7 * align_up(N * 4, 256);                              // vals_a, sa, rank, vals_b, cl0, cl1, sfhi
     b += align_up(N, 256);                                      // uflag
     b += align_up((size_t)nstreams * (cap + 8) * 2, 256);       // mtfv
     b += 2 * align_up((size_t)nstreams * sel_cap, 256);         // sel, sel_mtf
@@ -3254,6 +2993,7 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * kMaxAlpha * 4, 256);       // mtf_freq
     b += align_up((size_t)nstreams * 8 * 4, 256);               // inuse
     b += align_up((size_t)nstreams * kMaxGroups * 4 + 64, 256);  // wide heap list
+    b += align_up((size_t)nstreams * 512 * 4, 256);             // A / B rotations per first byte
     b += 16 * align_up((size_t)nstreams * 4 + 64, 256);         // small per-stream arrays
     b += align_up(((size_t)nstreams + 1) * 8 + 32, 256);        // offsets + counters
     b += align_up(prim_tmp_bytes(nstreams, cap), 256);          // rocPRIM temporary storage
@@ -3306,8 +3046,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.sel_cap = (uint32_t)align_up(B.cap / kGSize + 8, 64);
     B.level = level;
     B.nblock_max = 100000u * level - 19u;
-    static const uint32_t tie_direct = !(std::getenv("LFM_TIE_DIRECT") && std::atoi(std::getenv("LFM_TIE_DIRECT")) == 0);
-    B.tie_direct = tie_direct;
     if (ws_bytes < lfm_hip_bzip2_workspace_bytes(count, raw_cap)) return LFM_HIP_EINVAL;
     const size_t N = (size_t)count * B.cap;
     if (N >= (1ull << 32)) return LFM_HIP_EINVAL;
@@ -3324,6 +3062,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.cl0 = (uint32_t*)take(N * 4);
     B.cl1 = (uint32_t*)take(N * 4);
     B.uflag = take(N);
+    B.sfhi = (uint32_t*)take(N * 4);
     B.mtfv = (uint16_t*)take((size_t)count * (B.cap + 8) * 2);
     B.sel = take((size_t)count * B.sel_cap);
     B.sel_mtf = take((size_t)count * B.sel_cap);
@@ -3334,8 +3073,9 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.mtf_freq = (uint32_t*)take((size_t)count * kMaxAlpha * 4);
     B.inuse = (uint32_t*)take((size_t)count * 8 * 4);
     B.wide = (uint32_t*)take((size_t)count * kMaxGroups * 4 + 64);
+    B.abcnt = (uint32_t*)take((size_t)count * 512 * 4);
     uint32_t** small[] = {&B.raw_len, &B.n, &B.crc, &B.flags, &B.done, &B.seg_begin, &B.seg_end, &B.nmtf,
-                          &B.orig_ptr, &B.nsel, &B.ngroups, &B.out_bytes};
+                          &B.orig_ptr, &B.nsel, &B.ngroups, &B.out_bytes, &B.nsub, &B.bwt_mode};
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
     for (int k = (int)(sizeof(small) / sizeof(small[0])); k < 16; ++k) (void)take((size_t)count * 4 + 64);
     uint64_t* offs = (uint64_t*)take(((size_t)count + 1) * 8 + 32);
@@ -3363,8 +3103,17 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     uint32_t* d_cnt = (uint32_t*)(offs + count + 1);
     B.wide_cnt = d_cnt + 3;
     mark(1);
-    // round 0: every rotation by its 8-byte prefix (buckets, then chunk sorts)
-    {
+    // BWT: the B rotations sorted (round 0 = bucket pass + chunk sorts by the
+    // 8-byte prefix, then the tie rounds), every other rotation placed by
+    // bwt_induce.  Ties that would need prefix doubling (long repeats) restart
+    // the batch with every rotation sorted (B.it_full: doubling ranks every
+    // rotation), which also finds the periodic blocks.
+    uint32_t* cl = B.cl0;
+    uint32_t* cl_next = B.cl1;
+    uint32_t covered = kKeyBytes;
+    bool none_left = false;  // a count read 0 and no kernel ran since: skip the later reads
+    uint32_t first_ties = 0, left_runs = 0;  // tied slots after the chunk sorts, runs tie_runs_direct left (LFM_BZ2_STATS)
+    for (B.it_full = 0;; B.it_full = 1) {
         ChunkLists CL;
         const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
         for (int c = 0; c < 4; ++c) {
@@ -3377,59 +3126,16 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         if (hipMemsetAsync(d_cnt, 0, 32, st) != hipSuccess ||
             hipMemsetAsync(B.done, 0, (size_t)count * 4, st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
-        static const uint32_t bkt_bits = [] {
-            const int b = std::getenv("LFM_BKT_BITS") ? std::atoi(std::getenv("LFM_BKT_BITS")) : 0;
-            return b >= (int)kMinBucketBits && b <= (int)kMaxBucketBits ? (uint32_t)b : kBucketBits;
-        }();
-        if (bkt_bits == 13) hipLaunchKernelGGL(bwt_bucket<13>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
-        else if (bkt_bits == 15) hipLaunchKernelGGL(bwt_bucket<15>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
-        else hipLaunchKernelGGL(bwt_bucket<14>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
+        hipLaunchKernelGGL(bwt_bucket<kBucketBits>, dim3(count), dim3(kBucketThreads), 0, st, B, CL);
         if (!ok() || hipMemcpyAsync(nch, d_cnt, 24, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return LFM_HIP_ERUNTIME;
-        static const int cs_shape = std::getenv("LFM_CS_SHAPE") ? std::atoi(std::getenv("LFM_CS_SHAPE")) : 0;
-        static const int cs_xcd = std::getenv("LFM_CS_XCD") ? std::atoi(std::getenv("LFM_CS_XCD")) : 1;
-        // grid and chunks-per-XCD of a chunk list (XCD-aware order unless LFM_CS_XCD=0)
+        // chunks in XCD-aware order: workgroup b runs on XCD b % 8
         auto cs_grid = [&](uint32_t nc, uint32_t& per) {
-            per = cs_xcd ? (nc + 7) / 8 : 0u;
-            return dim3(cs_xcd ? 8 * per : nc);
+            per = (nc + 7) / 8;
+            return dim3(8 * per);
         };
         uint32_t per = 0;
-        // chunk sorts: the rocPRIM block merge sort below (default), or the
-        // hand-written ones (LFM_CS_ALGO=1 LDS merge path, 2 register bitonic;
-        // both measured slower)
-        static const int cs_algo = [] {
-            const char* e = std::getenv("LFM_CS_ALGO");
-            const int x = e ? std::atoi(e) : 0;
-            return x >= 0 && x <= 2 ? x : 0;
-        }();
-        if (cs_algo) {
-            const void* fk[3];
-            if (cs_algo == 2) {
-                fk[0] = (const void*)bwt_chunk_bsort<kTinyCap / 8>;
-                fk[1] = (const void*)bwt_chunk_bsort<kSmallCap / 8>;
-                fk[2] = (const void*)bwt_chunk_bsort<kBigCap / 8>;
-            } else {
-                fk[0] = (const void*)bwt_chunk_msort<kTinyCap / 8, 8>;
-                fk[1] = (const void*)bwt_chunk_msort<kSmallCap / 8, 8>;
-                fk[2] = (const void*)bwt_chunk_msort<kBigCap / 8, 8>;
-            }
-            const uint32_t cls_n[3] = {nch[5], nch[0], nch[1]};
-            uint32_t* const cls_b[3] = {CL.b[3], CL.b[0], CL.b[1]};
-            uint32_t* const cls_e[3] = {CL.e[3], CL.e[0], CL.e[1]};
-            const uint32_t cls_th[3] = {kTinyCap / 8, kSmallCap / 8, kBigCap / 8};
-            for (int q = 0; q < 3; ++q) {
-                if (!cls_n[q]) continue;
-                const void* f = fk[q];
-                const dim3 g = cs_grid(cls_n[q], per);
-                const uint32_t* cbq = cls_b[q];
-                const uint32_t* ceq = cls_e[q];
-                uint32_t nq = cls_n[q];
-                void* args[] = {&B, &cbq, &ceq, &nq, &per};
-                if (hipLaunchKernel(f, g, dim3(cls_th[q]), args, 0, st) != hipSuccess) return LFM_HIP_ERUNTIME;
-            }
-            nch[5] = nch[0] = nch[1] = 0;  // done: only the rocPRIM segmented class below
-        }
         if (nch[5]) {
             const dim3 g = cs_grid(nch[5], per);
             hipLaunchKernelGGL((bwt_chunk_sort<kTinyCap / kCsItems, kCsItems>), g, dim3(kTinyCap / kCsItems), 0, st, B,
@@ -3437,50 +3143,32 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         }
         if (nch[0]) {
             const dim3 g = cs_grid(nch[0], per);
-            if (cs_shape == 1)  // 1024 threads x 2 items (same capacity)
-                hipLaunchKernelGGL((bwt_chunk_sort<2 * kCsThreads, kCsItems / 2>), g, dim3(2 * kCsThreads), 0, st, B,
-                                   CL.b[0], CL.e[0], nch[0], per);
-            else if (cs_shape == 2)  // 256 threads x 8 items
-                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads / 2, kCsItems * 2>), g, dim3(kCsThreads / 2), 0, st, B,
-                                   CL.b[0], CL.e[0], nch[0], per);
-            else
-                hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), g, dim3(kCsThreads), 0, st, B, CL.b[0],
-                                   CL.e[0], nch[0], per);
+            hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), g, dim3(kCsThreads), 0, st, B, CL.b[0], CL.e[0],
+                               nch[0], per);
         }
         if (nch[1]) {
             const dim3 g = cs_grid(nch[1], per);
-            static const int big_shape = std::getenv("LFM_BIG_SHAPE") ? std::atoi(std::getenv("LFM_BIG_SHAPE")) : 0;
-            if (big_shape == 1)  // 1024 threads x 4 items (same capacity; measured equal to 512 x 8)
-                hipLaunchKernelGGL((bwt_chunk_sort<2 * kBigThreads, kBigItems / 2>), g, dim3(2 * kBigThreads), 0, st, B,
-                                   CL.b[1], CL.e[1], nch[1], per);
-            else
-                hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
-                                   CL.e[1], nch[1], per);
+            hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
+                               CL.e[1], nch[1], per);
         }
         if (nch[2]) {
             hipLaunchKernelGGL(bwt_chunk_keys, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
             e = rocprim::segmented_radix_sort_pairs(tmp, tmp_bytes, B.keys_a, B.keys_b, B.vals_a, B.sa, (unsigned)N,
-                                                    nch[2], CL.b[2], CL.e[2], 0, 64 - bkt_bits, st);
+                                                    nch[2], CL.b[2], CL.e[2], 0, 64 - kBucketBits, st);
             if (e == hipSuccess)
                 hipLaunchKernelGGL(bwt_chunk_flags, dim3(nch[2]), dim3(256), 0, st, B, CL.b[2], CL.e[2]);
         }
         if (!ok()) return LFM_HIP_ERUNTIME;
-    }
-    uint32_t* cl = B.cl0;
-    uint32_t* cl_next = B.cl1;
-    if (e == hipSuccess) {
+        cl = B.cl0;
+        cl_next = B.cl1;
         hipLaunchKernelGGL(tie_offsets, dim3(1), dim3(1024), 0, st, B, d_cnt);
         hipLaunchKernelGGL(tie_compact, dim3(count), dim3(256), 0, st, B, B.cl0);
-        if (B.tie_direct) hipLaunchKernelGGL(tie_runs_direct, dim3(1024), dim3(256), 0, st, B, B.cl0, d_cnt, d_cnt + 7);
+        hipLaunchKernelGGL(tie_runs_direct, dim3(1024), dim3(256), 0, st, B, B.cl0, d_cnt, d_cnt + 7);
         if (!ok()) return LFM_HIP_ERUNTIME;
-    }
-    uint32_t covered = kKeyBytes;
-    uint32_t* d_cnt2 = d_cnt + 1;
-    // text rounds over the tied list (group keys: u64 per entry in the rank
-    // area, group index / bounds in the mtfv area -- both free here)
-    bool none_left = false;  // a count read 0 and no kernel ran since: skip the later reads
-    uint32_t first_ties = 0, left_runs = 0;  // tied slots after the chunk sorts, runs tie_runs_direct left (LFM_BZ2_STATS)
-    {
+        covered = kKeyBytes;
+        none_left = false;
+        // text rounds over the tied list (group keys: u64 per entry in the rank
+        // area, group index / bounds in the mtfv area -- both free here)
         uint64_t* gk = (uint64_t*)B.rank;
         uint32_t* bnd = (uint32_t*)B.mtfv;
         for (int r = 0; r < kTextRounds && e == hipSuccess; ++r) {
@@ -3496,7 +3184,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
                 first_ties = cnt;
                 left_runs = c8[7];
             }
-            if (cnt == 0 || (r == 0 && B.tie_direct && c8[7] == 0)) {  // nothing tied, or tie_runs_direct sorted every run
+            if (cnt == 0 || (r == 0 && c8[7] == 0)) {  // nothing tied, or tie_runs_direct sorted every run
                 none_left = true;
                 break;
             }
@@ -3518,42 +3206,44 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
             if (e != hipSuccess) break;
             hipLaunchKernelGGL(text_write, dim3(grid), dim3(256), 0, st, B, cl, d_cnt);
             covered += tb;
-            e = rocprim::select(tmp, tmp_bytes, B.keys_b, B.uflag, gk, d_cnt2, (size_t)cnt, st);
+            e = rocprim::select(tmp, tmp_bytes, B.keys_b, B.uflag, gk, d_cnt + 1, (size_t)cnt, st);
             if (e == hipSuccess) e = rocprim::select(tmp, tmp_bytes, cl, B.uflag, cl_next, d_cnt, (size_t)cnt, st);
             std::swap(cl, cl_next);
         }
-        // ties left (long repeats): ranks of every rotation for doubling
+        if (e != hipSuccess) return LFM_HIP_ERUNTIME;
+        // ties left (long repeats)
         uint32_t cnt = 0;
-        if (e == hipSuccess && !none_left &&
-            (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-             hipStreamSynchronize(st) != hipSuccess))
-            e = hipErrorUnknown;
-        if (e == hipSuccess && cnt > 0) {
-            // group bounds of the remaining list: from the last text keys, or
-            // from the first-round keys when no text round ran
-            uint64_t* gsrc = gk;
-            const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
-            if (covered == kKeyBytes) {
-                gsrc = (uint64_t*)B.vals_b;  // cnt * 8 <= N * 4 when cnt <= N / 2: fall back to rank0 otherwise
-            }
-            if (covered == kKeyBytes && (size_t)cnt * 2 > N) {
-                hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B);
-            } else {
-                if (covered == kKeyBytes)
-                    hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gsrc);
-                uint32_t* bnd2 = (uint32_t*)B.keys_a;  // 2 * cnt u32 fit the keys area
-                uint32_t* hv = bnd2 + cnt;
-                uint32_t* hvs = (uint32_t*)B.cl1 == cl ? (uint32_t*)B.cl0 : (uint32_t*)B.cl1;
-                hipLaunchKernelGGL(text_bounds, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gsrc, bnd2);
-                hipLaunchKernelGGL(text_head_slots, dim3(grid), dim3(256), 0, st, cl, d_cnt, bnd2, hv);
-                e = rocprim::inclusive_scan(tmp, tmp_bytes, hv, hvs, (size_t)cnt, rocprim::maximum<uint32_t>(), st);
-                hipLaunchKernelGGL(bwt_rank_all, dim3(8192), dim3(256), 0, st, B, N);
-                hipLaunchKernelGGL(text_rank_tied, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, hvs);
-                cl_next = hvs == (uint32_t*)B.cl0 ? B.cl0 : B.cl1;
-            }
+        if (!none_left && (hipMemcpyAsync(&cnt, d_cnt, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                           hipStreamSynchronize(st) != hipSuccess))
+            return LFM_HIP_ERUNTIME;
+        if (cnt == 0) {
+            none_left = true;
+            break;
         }
+        if (!B.it_full) continue;  // doubling needs the rank of every rotation: sort them all
+        // ranks of every rotation for doubling: group bounds of the remaining
+        // list from the last text keys, or from the first-round keys when no
+        // text round ran
+        uint64_t* gsrc = gk;
+        const uint32_t grid = std::min<uint32_t>(4096, (cnt + 255) / 256);
+        if (covered == kKeyBytes) gsrc = (uint64_t*)B.vals_b;  // cnt * 8 <= N * 4 when cnt <= N / 2: rank0 otherwise
+        if (covered == kKeyBytes && (size_t)cnt * 2 > N) {
+            hipLaunchKernelGGL(bwt_rank0, dim3(count), dim3(1024), 0, st, B);
+        } else {
+            if (covered == kKeyBytes) hipLaunchKernelGGL(text_gather_keys, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gsrc);
+            uint32_t* bnd2 = (uint32_t*)B.keys_a;  // 2 * cnt u32 fit the keys area
+            uint32_t* hv = bnd2 + cnt;
+            uint32_t* hvs = (uint32_t*)B.cl1 == cl ? (uint32_t*)B.cl0 : (uint32_t*)B.cl1;
+            hipLaunchKernelGGL(text_bounds, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, gsrc, bnd2);
+            hipLaunchKernelGGL(text_head_slots, dim3(grid), dim3(256), 0, st, cl, d_cnt, bnd2, hv);
+            e = rocprim::inclusive_scan(tmp, tmp_bytes, hv, hvs, (size_t)cnt, rocprim::maximum<uint32_t>(), st);
+            hipLaunchKernelGGL(bwt_rank_all, dim3(8192), dim3(256), 0, st, B, N);
+            hipLaunchKernelGGL(text_rank_tied, dim3(grid), dim3(256), 0, st, B, cl, d_cnt, hvs);
+            cl_next = hvs == (uint32_t*)B.cl0 ? B.cl0 : B.cl1;
+        }
+        break;
     }
-    // doubling rounds over what the text rounds left (long repeats only)
+    // doubling rounds over what the text rounds left (long repeats only, B.it_full)
     uint32_t h = covered;
     const uint32_t max_n = B.cap;
     while (e == hipSuccess && !none_left) {
@@ -3583,6 +3273,14 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         h *= 2;
     }
     if (e != hipSuccess) return LFM_HIP_ERUNTIME;
+    if (!B.it_full) {
+        // the other type placed by one scan; the final order in the vals_b area
+        B.sfin = B.vals_b;
+        hipLaunchKernelGGL(bwt_place_sorted, dim3(count), dim3(256), 0, st, B);
+        hipLaunchKernelGGL(bwt_induce, dim3(count), dim3(64), 0, st, B);
+        if (!ok()) return LFM_HIP_ERUNTIME;
+        B.sa = B.sfin;
+    }
     mark(2);
     if (t_hook) t_hook(t_hook_ctx, 1);  // the doubling / tie rounds above end with a host synchronisation
     {
@@ -3591,11 +3289,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         const dim3 g((nseg_max + 3) / 4, count);
         hipLaunchKernelGGL(mtf_last, g, dim3(256), 0, st, B, nseg_max, seg_last);
         hipLaunchKernelGGL(mtf_prefix, dim3(count), dim3(256), 0, st, B, nseg_max, seg_last);
-        static const bool seq_mtf = std::getenv("LFM_MTF") && std::strcmp(std::getenv("LFM_MTF"), "seq") == 0;
-        if (seq_mtf)
-            hipLaunchKernelGGL(mtf_seg, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
-        else
-            hipLaunchKernelGGL(mtf_win, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
+        hipLaunchKernelGGL(mtf_win, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
         hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
     }
     // streams whose Huffman weights need u64 heap entries (listed by rle2)
@@ -3605,43 +3299,15 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         return LFM_HIP_ERUNTIME;
     mark(3);
     if (t_hook) t_hook(t_hook_ctx, 2);  // after the wide-stream count's synchronisation: rle2 has run
-    static const bool hsel = !(std::getenv("LFM_HSEL") && std::atoi(std::getenv("LFM_HSEL")) == 0);
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
     for (int it = 0; it < kIters; ++it) {
-        if (hsel) hipLaunchKernelGGL(huff_select_reg, dim3(count), dim3(kHuffThreads), 0, st, B);
-        else hipLaunchKernelGGL(huff_select, dim3(count), dim3(kHuffThreads), 0, st, B);
-        static const int lanes = [] {
-            const char* v = std::getenv("LFM_HUFF_LANES");
-            const int x = v ? std::atoi(v) : kLenTasks;
-            return (x == 1 || x == 2 || x == 4 || x == 8 || x == 16) ? x : kLenTasks;
-        }();
-        // uniform heaps, u32 entries for the narrow tables and u64 for the
-        // streams rle2 listed, in one launch (LFM_HUFF_PACK = heaps per
-        // workgroup, 32 by default; 0 = the per-lane branchy kernel below)
-        static const int plane = [] {
-            const char* v = std::getenv("LFM_HUFF_PACK");
-            const int x = v ? std::atoi(v) : 32;
-            return (x == 0 || x == 4 || x == 8 || x == 16 || x == 32) ? x : 32;
-        }();
-        const dim3 g((count * kMaxGroups + lanes - 1) / lanes);
-        if (plane) {
-            const uint32_t nn = (count * kMaxGroups + plane - 1) / plane;
-            const uint32_t nw = (nwide * kMaxGroups + plane / 2 - 1) / (plane / 2);
-            switch (plane) {
-            case 4: hipLaunchKernelGGL(huff_lengths_heap<4>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
-            case 8: hipLaunchKernelGGL(huff_lengths_heap<8>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
-            case 32: hipLaunchKernelGGL(huff_lengths_heap<32>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
-            default: hipLaunchKernelGGL(huff_lengths_heap<16>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide); break;
-            }
-        } else {
-            switch (lanes) {
-            case 1: hipLaunchKernelGGL(huff_lengths<1>, g, dim3(64), 0, st, B); break;
-            case 2: hipLaunchKernelGGL(huff_lengths<2>, g, dim3(64), 0, st, B); break;
-            case 4: hipLaunchKernelGGL(huff_lengths<4>, g, dim3(64), 0, st, B); break;
-            case 8: hipLaunchKernelGGL(huff_lengths<8>, g, dim3(64), 0, st, B); break;
-            default: hipLaunchKernelGGL(huff_lengths<16>, g, dim3(64), 0, st, B); break;
-            }
-        }
+        hipLaunchKernelGGL(huff_select_reg, dim3(count), dim3(kHuffThreads), 0, st, B);
+        // uniform heaps, 32 per workgroup: u32 entries for the narrow tables,
+        // u64 for the streams rle2 listed, in one launch
+        constexpr uint32_t kPlane = 32;
+        const uint32_t nn = (count * kMaxGroups + kPlane - 1) / kPlane;
+        const uint32_t nw = (nwide * kMaxGroups + kPlane / 2 - 1) / (kPlane / 2);
+        hipLaunchKernelGGL(huff_lengths_heap<kPlane>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide);
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
     mark(4);

@@ -202,6 +202,7 @@ int MemSink::append(const uint8_t* p, size_t n)
 uint8_t* MemSink::direct(size_t n)
 {
     const size_t at = out_->size();
+    if (at + n > out_->capacity() && worst_ > at + n && !out_->reserve(worst_)) return nullptr;
     if (!out_->resize(at + n)) return nullptr;
     return out_->data() + at;
 }
@@ -798,7 +799,11 @@ int Encoder::start_upload(const void* img, klb_image_header& h, const SlabSpec& 
     cz = std::min<uint64_t>(cz, Z);
     const uint64_t per_vol = (Z + cz - 1) / cz, nch = V * per_vol;
     const size_t cbytes = cz * fs;
-    const uint64_t nslot = std::min<uint64_t>(nch, std::max<uint64_t>(2, ring_target / cbytes));
+    // at least 3 slots: the SDMA loop issues copy c before chunk c - 1 is
+    // predicted, and slot c % nslot must no longer be read by chunk
+    // c - nslot + 1 (its last frame is that chunk's temporal predecessor), so
+    // that chunk's predictor must already be issued when copy c waits for it
+    const uint64_t nslot = std::min<uint64_t>(nch, std::max<uint64_t>(3, ring_target / cbytes));
     if (!dev_alloc(d_in_, d_in_cap_, nslot * cbytes)) return 3;
     if (!dev_alloc(d_sym_[set], d_sym_cap_[set], V * Z * fs)) return 3;
     while (up.ev.size() < 3 * nch) {
@@ -1320,7 +1325,11 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     // host stack still uploading (start_upload): a batch waits for the chunks
     // holding its last block (blocks run x -> y -> z -> c -> t, so that block
     // reaches furthest into the flattened (t, c, z) frame order)
-    UploadPipe* up = up_[set].active ? &up_[set] : nullptr;
+    UploadPipe* up = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(up_[set].mu);
+        if (up_[set].active) up = &up_[set];
+    }
     auto frames_needed = [&](uint64_t last_block) -> uint64_t {
         uint64_t o[5], sz[5];
         g.block(last_block, o, sz);

@@ -65,6 +65,7 @@ public:
     uint8_t* data() { return p_; }
     const uint8_t* data() const { return p_; }
     size_t size() const { return size_; }
+    size_t capacity() const { return cap_; }
 private:
     uint8_t* p_ = nullptr;
     size_t size_ = 0, cap_ = 0;
@@ -90,16 +91,19 @@ public:
     uint8_t* direct(size_t n) override;
     // n is the worst case (every block stored at its raw size + bzip2's
     // overhead); beyond 8 GiB only 60 % of it is pinned up front (ratio >= 1.67
-    // fits; a worse one grows the buffer by half again, with a copy): a
-    // 100-volume config-5 stack (107 GB raw, 52 GB .lfm) would otherwise pin
-    // 110 GB of host memory for its output
+    // fits): a 100-volume config-5 stack (107 GB raw, 52 GB .lfm) would
+    // otherwise pin 110 GB of host memory for its output.  A stack that
+    // compresses worse grows the buffer once, straight to the worst case
+    // (direct()), so the peak is the old buffer plus n, never more.
     void reserve_hint(size_t n) override
     {
         const size_t big = (size_t)8 << 30;
+        worst_ = n;
         (void)out_->reserve(n <= big ? n : std::max(big, n / 10 * 6));
     }
 private:
     PinnedBuffer* out_;
+    size_t worst_ = 0;
 };
 
 // Compress every block of `sym` (image layout, bpp bytes per pixel) in

@@ -126,7 +126,7 @@ def lib():
     L.lfm_free.argtypes = [vp]
     L.lfm_free.restype = None
     L.lfm_decode_memory.argtypes = [ctypes.c_char_p, ctypes.c_uint64, vp, ctypes.c_int]
-    L.lfm_decode_memory_roi.argtypes = [vp, ctypes.c_uint64, u32p, u32p, vp, ctypes.c_int]
+    L.lfm_decode_memory_roi.argtypes = [vp, ctypes.c_uint64, u32p, u32p, vp, ctypes.c_uint64, ctypes.c_int]
     L.lfm_hip_predict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_unpredict.argtypes = [vp, vp, vp] + [ctypes.c_int] * 8 + [vp]
     L.lfm_hip_predict_candidates.argtypes = [vp, vp] + [ctypes.c_int] * 4 + [vp]
@@ -486,23 +486,31 @@ def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):
     return out
 
 
-def decode_roi(buf, lb, ub, dtype=np.uint16, num_threads=-1, out=None):
+def decode_roi(buf, lb, ub, dtype=None, num_threads=-1, out=None):
     """Region lb .. ub (inclusive, [x, y, z, c, t]) of an in-memory .lfm
-    (lfm_decode_memory_roi); returns an array [t, c, z, y, x] of the region.
-    `out` (optional): a C-contiguous array of the region's size and dtype to
-    decode into (readKLBroiInPlace's caller-owned buffer), returned reshaped."""
+    (lfm_decode_memory_roi); returns an array [t, c, z, y, x] of the region in
+    the file's data type (header byte 42).  `dtype`, when given, must be that
+    type.  `out` (optional): a C-contiguous array of the region's size and the
+    file's dtype to decode into (readKLBroiInPlace's caller-owned buffer),
+    returned reshaped.  The library checks the byte count as well."""
+    if len(buf) < 43:
+        raise ValueError("decode_roi: %d bytes hold no .lfm header" % len(buf))
+    if buf[42] not in NP_OF:
+        raise ValueError("decode_roi: unknown data type %d in the header" % buf[42])
+    fdt = np.dtype(NP_OF[buf[42]])
+    if dtype is not None and np.dtype(dtype) != fdt:
+        raise ValueError("decode_roi: the file holds %s, not %s" % (fdt, np.dtype(dtype)))
     shape = tuple(int(u) - int(l) + 1 for l, u in zip(lb, ub))[::-1]
     if out is None:
-        out = np.empty(shape, dtype=dtype)
+        out = np.empty(shape, dtype=fdt)
     else:
         if not isinstance(out, np.ndarray) or not out.flags.c_contiguous or not out.flags.writeable:
             raise ValueError("decode_roi: out must be a writeable C-contiguous numpy array")
-        if out.dtype != np.dtype(dtype) or out.size != int(np.prod(shape)):
-            raise ValueError("decode_roi: out holds %d x %s, the region is %s x %s"
-                             % (out.size, out.dtype, shape, np.dtype(dtype)))
+        if out.dtype != fdt or out.size != int(np.prod(shape)):
+            raise ValueError("decode_roi: out holds %d x %s, the region is %s x %s" % (out.size, out.dtype, shape, fdt))
         out = out.reshape(shape)
-    _check(lib().lfm_decode_memory_roi(_addr(buf), len(buf), _u32(lb), _u32(ub), out.ctypes.data, num_threads),
-           "lfm_decode_memory_roi")
+    _check(lib().lfm_decode_memory_roi(_addr(buf), len(buf), _u32(lb), _u32(ub), out.ctypes.data, out.nbytes,
+                                       num_threads), "lfm_decode_memory_roi")
     return out
 
 

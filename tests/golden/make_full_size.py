@@ -50,7 +50,52 @@ CONFIGS = {
     # volume_sha256[t] = SHA-256 of volume t's block streams
     "cfg5x4_4096x4096x32x1x4_video_tiles_auto": (4096, 4096, 32, 13, "tiles", 0x80, 0x4C464D05, 4),
 }
+# config 5, far t-volumes of the 100-volume stack (4096 x 4096 x 32 x 1 x 100):
+# volume_sha256[t] for t in FAR_VOLUMES, each volume's block streams coded
+# alone with the predictor chosen on volume 0's frame 0.  In the 100-volume
+# .lfm (51.6 GB) these streams sit at end-offsets far past 2^32, so checking
+# them checks the u64 offset table (klb_imageHeader.h:46) as well.
+FAR_NAME = "cfg5far_4096x4096x32x1x100_video_tiles_auto"
+FAR_VOLUMES = (50, 99)
 BLOCK = [96, 96, 8, 1, 1]  # default uint16 block (klb_imageHeader.cpp:301-309)
+
+
+def volume_digests(X, Y, Z, T, family, hv, seed, threads, ts):
+    """SHA-256 and byte count of the block streams of t-volumes `ts` of the
+    video stack (volume t alone, predictor chosen on volume 0's frame 0)."""
+    bz = O.bzip2()
+    assert "reference" in bz.kind, "build oracle/_ref first (make -C oracle)"
+    video = hv >> 7
+    f0 = O.synthetic_lf(X, Y, Z=1, T=T, seed=seed)[0, 0, 0]
+    k, _ = O.select(f0, T, family)
+    bs = [min(b, x) for b, x in zip(BLOCK, [X, Y, Z, 1, 1])]
+    level = min(9, -(-2 * int(np.prod(bs)) // 100000))
+    nbx, nby = math.ceil(X / bs[0]), math.ceil(Y / bs[1])
+    out = {}
+    with ThreadPoolExecutor(threads) as ex:
+        for t in ts:
+            h, n, prev_raw = hashlib.sha256(), 0, None
+            for z0 in range(0, Z, bs[2]):
+                dz = min(bs[2], Z - z0)
+                raw = O.synthetic_lf(X, Y, Z=dz, T=T, seed=seed, z0=z0, t0=t, idx0=(t * Z + z0) * X * Y)[0, 0]
+                sym = np.empty_like(raw)
+                for j in range(dz):
+                    z = z0 + j
+                    zf = (video & z) & 1
+                    p = raw[j - 1] if j else prev_raw
+                    sym[j] = O.predict_frame(raw[j], p if zf else None, T, family, k, zf) if k else raw[j]
+                prev_raw = raw[-1].copy()
+
+                def one(b):
+                    by, bx = divmod(b, nbx)
+                    blk = np.ascontiguousarray(sym[:, by * bs[1]:(by + 1) * bs[1], bx * bs[0]:(bx + 1) * bs[0]])
+                    return bz.compress(blk.tobytes(), level)
+                for blob in ex.map(one, range(nbx * nby)):
+                    h.update(blob)
+                    n += len(blob)
+            out[str(t)] = dict(sha256=h.hexdigest(), bytes=n)
+    return dict(chosen=int(k), final_header_version=(hv & 0x80) | int(k), level=level,
+                nblocks_per_volume=nbx * nby * math.ceil(Z / bs[2]), volumes=out)
 
 
 def encode_full(X, Y, Z, T, family, hv, seed, threads, Tn=1):
@@ -130,6 +175,15 @@ def main():
         man[name] = e
         print("%s: %d bytes, predictor %d, ratio %.3f, %.1f s" % (name, e["size"], e["chosen"], e["ratio"],
                                                                   time.time() - t0), flush=True)
+    if not args.only or args.only == FAR_NAME:
+        t0 = time.time()
+        X, Y, Z, T, fam, hv, seed = 4096, 4096, 32, 13, "tiles", 0x80, 0x4C464D05
+        r = volume_digests(X, Y, Z, T, fam, hv, seed, args.threads, FAR_VOLUMES)
+        man[FAR_NAME] = dict(name=FAR_NAME, xyzct=[X, Y, Z, 1, 100], nnum=T, family=fam, header_version=hv,
+                             seed=seed, block_size=BLOCK, bzip2=O.bzip2().kind,
+                             generator="synthetic_lf(%d,%d,%d,T=%d,seed=0x%X, t0=t, idx0=t*Z*X*Y) per volume"
+                             % (X, Y, Z, T, seed), **r)
+        print("%s: volumes %s, %.1f s" % (FAR_NAME, list(FAR_VOLUMES), time.time() - t0), flush=True)
     with open(path, "w") as f:
         json.dump(list(man.values()), f, indent=1)
 

@@ -366,6 +366,24 @@ def _bz2_cases():
     geo = np.minimum(rng.geometric(0.5, 140000) - 1, 40).astype(np.uint8)
     cases["geometric"] = geo
     cases["geometric_small"] = geo[:30000].copy()
+    # two-stage BWT (bwt_induce): descending runs make chains of A rotations
+    # longer than the four carried bytes (the text fallback); bytes in threes
+    # (RLE1 keeps them) make A rotations induce into their own bucket, mostly
+    # into the same 64-position slice; a long run of 0xFB survives RLE1 as a
+    # run of equal bytes, leaving types undecided (the stream is sorted whole);
+    # 8-bit text-like data
+    desc = []
+    while sum(len(d) for d in desc) < 60000:
+        a = int(rng.integers(20, 256))
+        desc.append(np.arange(a, a - int(rng.integers(3, 20)), -1).astype(np.uint8))
+        desc.append(rng.integers(0, 256, int(rng.integers(0, 3)), dtype=np.uint8))
+    cases["descending"] = np.concatenate(desc)
+    cases["ascending"] = np.concatenate([np.arange(a, min(256, a + 12)) for a in rng.integers(0, 250, 6000)]).astype(np.uint8)
+    cases["threes"] = np.repeat(rng.integers(0, 40, 20000, dtype=np.uint8), 3)
+    cases["fb_runs"] = np.concatenate([np.full(3000, 0xFB, np.uint8), rng.integers(0, 256, 5000, dtype=np.uint8),
+                                       np.full(1300, 0xFB, np.uint8), np.array([1, 0xFB, 2], np.uint8)])
+    words = [bytes(rng.integers(97, 123, int(rng.integers(1, 9)), dtype=np.uint8)) for _ in range(400)]
+    cases["text"] = np.frombuffer(b" ".join(words[int(i)] for i in rng.integers(0, 400, 12000)), np.uint8).copy()
     return cases
 
 
@@ -384,6 +402,27 @@ def test_gpu_bzip2_matches_libbz2_edge_cases(lfmlib, oracle, gpu):
                 continue
             assert not name.startswith("periodic"), name
             assert got[0] == exp, (name, level, len(got[0]), len(exp))
+
+
+@pytest.mark.parametrize("repeats", [False, True])
+def test_gpu_bzip2_mixed_batch(lfmlib, oracle, gpu, repeats):
+    """The edge cases as the streams of ONE batch (padded to a common length
+    with distinct random tails): induced and whole-sorted streams and host
+    fallbacks side by side; with the long repeats, ties that need doubling
+    restart the batch with every rotation sorted."""
+    torch = gpu
+    rng = np.random.default_rng(5)
+    slow = ("long_repeat", "tie_past", "motif", "periodic")
+    cases = [c for k, c in _bz2_cases().items() if len(c) <= 100000 and (repeats or not k.startswith(slow))]
+    n = max(len(c) for c in cases) + 64
+    img = np.stack([np.concatenate([c, rng.integers(0, 256, n - len(c), dtype=np.uint8)]) for c in cases])
+    d = torch.from_numpy(img.reshape(-1).copy()).cuda()
+    got, flags = lfmlib.bzip2_device(d, [n, 1, len(cases), 1, 1], [n, 1, 1, 1, 1], 1, level=2)
+    for i in range(len(cases)):
+        exp = ref_bz2(oracle, img[i].tobytes(), 2)
+        if flags[i]:
+            continue
+        assert got[i] == exp, i
 
 
 def test_gpu_bzip2_block_grid_and_symbols(lfmlib, oracle, gpu):
@@ -637,7 +676,8 @@ torch.cuda.set_device(0)
 out = {}
 enc = lfm.Encoder(device=0)
 # 1. tiles video stack: 1-MiB chunks (4 frames of 512 x 256), a 2-MiB ring
-#    (2 slots: every slot reused, temporal predecessors across chunk edges)
+#    (3 slots, the minimum: every slot reused, temporal predecessors across
+#    chunk edges)
 img = O.synthetic_lf(512, 256, Z=21, T=13, seed=41)
 lfm.set_family("tiles")
 out["video"] = enc.encode(img, header_version=0x80, nnum=13)[0] == O.encode(img, header_version=0x80, nnum=13,
@@ -647,8 +687,9 @@ img5 = O.synthetic_lf(520, 200, Z=5, C=2, Tn=3, T=15, seed=42)
 out["5d"] = enc.encode(img5, header_version=8 + 5, nnum=15, block_size=[64, 64, 2, 1, 1])[0] == O.encode(
     img5, header_version=8 + 5, nnum=15, family="tiles", block_size=[64, 64, 2, 1, 1])
 # 3. a z-slab of a video stack starting at an odd frame, host input: its
-#    previous raw frame comes from the host
-full = O.synthetic_lf(512, 256, Z=17, T=13, seed=43)[0, 0]
+#    previous raw frame comes from the host; the second slab's 24 frames are
+#    6 chunks, so the ring's slots are reused under the odd-start pairing
+full = O.synthetic_lf(512, 256, Z=33, T=13, seed=43)[0, 0]
 k, _ = lfm.select_device(torch.from_numpy(full[0].view(np.int16)).cuda(), 512, 256, 13, "tiles")
 bs = [64, 64, 3, 1, 1]
 a, _ = enc.encode_slab(full[:9], 0, header_version=0x80 | (8 + k), nnum=13, block_size=bs)
@@ -678,7 +719,7 @@ print(json.dumps(out))
 def test_host_upload_pipe_chunks_and_ring(gpu, tmp_path):
     """Host stacks upload in chunks through a ring of device slots, each chunk
     predicted as it lands and every GPU-bzip2 batch waiting only for its
-    chunks (UploadPipe).  With 1-MiB chunks and a 2-slot ring every slot is
+    chunks (UploadPipe).  With 1-MiB chunks and a 3-slot ring every slot is
     reused: video stacks (temporal predecessors across chunk edges), 5-D
     stacks, an odd-start video slab with its previous frame from the host, and
     pipelined host submits (the stack refilled as soon as submit returns)

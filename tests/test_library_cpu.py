@@ -233,6 +233,33 @@ def test_decode_memory_roi_into_caller_buffer(lfmlib):
         lfmlib.decode_roi(b, [0, 0, 0, 0, 0], [9, 9, 0, 0, 0], out=np.zeros((10, 10), np.int32))
 
 
+def test_decode_roi_uses_the_file_dtype(lfmlib, tmp_path):
+    """decode_roi sizes its output from the header's data type (a uint32 or
+    float32 .lfm read with default arguments), refuses an explicit dtype the
+    file does not hold, and lfm_decode_memory_roi refuses an output buffer
+    smaller than region x bytes per pixel instead of writing past it."""
+    import ctypes
+    rng = np.random.default_rng(3)
+    for dt in (np.uint32, np.float32):
+        img = (rng.integers(0, 1 << 20, (3, 20, 24)) if dt == np.uint32 else rng.random((3, 20, 24))).astype(dt)
+        p = tmp_path / ("roi_%s.klb" % np.dtype(dt).name)
+        lfmlib.write_klb(p, img)
+        b = open(p, "rb").read()
+        got = lfmlib.decode_roi(b, [2, 3, 1, 0, 0], [20, 17, 2, 0, 0])
+        assert got.dtype == dt
+        assert np.array_equal(got.reshape(2, 15, 19), img[1:3, 3:18, 2:21])
+        with pytest.raises(ValueError):
+            lfmlib.decode_roi(b, [0, 0, 0, 0, 0], [3, 3, 0, 0, 0], dtype=np.uint16)
+        small = np.zeros(16, np.uint16)  # 4 x 4 pixels of 4 bytes need 64 bytes, not 32
+        arr5 = (ctypes.c_uint32 * 5)
+        rc = lfmlib.lib().lfm_decode_memory_roi(b, len(b), arr5(0, 0, 0, 0, 0), arr5(3, 3, 0, 0, 0),
+                                                small.ctypes.data, small.nbytes, 1)
+        assert rc == 3 and not small.any()
+        rc = lfmlib.lib().lfm_decode_memory_roi(b, len(b), arr5(0, 0, 0, 0, 0), arr5(24, 3, 0, 0, 0),
+                                                small.ctypes.data, 1 << 20, 1)
+        assert rc == 3  # x = 24 is outside the 24-pixel rows
+
+
 def test_invalid_predictor_request_rejected(lfmlib, tmp_path):
     img = np.zeros((1, 16, 16), np.uint16)
     with pytest.raises(lfmlib.LfmError, match="code 6"):
@@ -287,3 +314,37 @@ def test_band5_release_wait_covers_the_round_stores():
     assert {n for _, n in waits} == {2, 3}, res           # both the spatial and the temporal wait
     assert len({k for k, _ in waits}) == 3, res           # in each family's kernel
     assert all(ops >= n for _, n, ops in res), res
+
+
+def test_header_u64_offsets_past_4gib(oracle, tmp_path):
+    """Block end-offsets past 2^32 (a 100-volume config-5 .lfm is 51.6 GB):
+    liblfm's klb_image_header writes them as u64 (klb_imageHeader.h:46,
+    klb_imageIO.cpp:1215-1217) and reads them back through readHeader,
+    parseHeader and readKLBheader (tests/c/header_u64.cpp); the header bytes
+    equal the oracle's and, when built, the reference class's own."""
+    import ctypes
+    import subprocess
+    exe = os.path.join(REPO, "tests", "c", "header_u64")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(REPO, "tests", "c")], check=True, capture_output=True)
+    path = str(tmp_path / "h64.lfm")
+    r = subprocess.run([exe, path], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    b = open(path, "rb").read()
+    xyzct, bs = [4096, 4096, 32, 1, 100], [96, 96, 8, 1, 1]
+    nb = 43 * 43 * 4 * 100
+    i = np.arange(nb, dtype=np.uint64)
+    offs = np.cumsum(70000 + (i * 7919) % 5003).astype(np.uint64)
+    assert int(offs[-1]) > 1 << 32 and len(b) == 320 + 8 * nb
+    assert np.array_equal(np.frombuffer(b, "<u8", nb, 320), offs)
+    md = b"u64 offsets".ljust(256, b"\0")
+    assert b == oracle.header_bytes(0x84, 13, xyzct, [1, 1, 2.5, 1, 1], 1, 1, md, bs, offs)
+    ref = os.path.join(REPO, "oracle", "_ref", "libklbheader_ref.so")
+    if os.path.exists(ref):
+        L = ctypes.CDLL(ref)
+        out = ctypes.create_string_buffer(len(b) + 64)
+        n = L.ref_header_bytes((ctypes.c_uint32 * 5)(*xyzct), 1, (ctypes.c_float * 5)(1, 1, 2.5, 1, 1),
+                               (ctypes.c_uint32 * 5)(*bs), 1, md, 0x84, 13,
+                               offs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ctypes.c_size_t(nb), out,
+                               len(b) + 64)
+        assert n == len(b) and out.raw[:n] == b
