@@ -433,6 +433,19 @@ bool gpu_bzip2_enabled()
     return on;
 }
 
+// GPU bzip2 for an encode: on unless disabled (LFM_GPU_BZIP2=0), not bzip2 or
+// no device; a host image of at most kHostBz2Bytes goes to the host library
+// (its predictor stage, if any, still runs on the GPU): a GPU batch costs
+// about a millisecond of launches and host synchronisations, more than
+// libbzip2 needs on the host threads for such an image (config 1's
+// 101 x 151 page: 1.3 ms through the GPU batch, 0.18 ms on the host).
+constexpr uint64_t kHostBz2Bytes = 1u << 20;
+static bool use_gpu_bzip2(const klb_image_header& h, bool dev)
+{
+    if (!gpu_bzip2_enabled() || h.compressionType != BZIP2 || lfm_hip_device_count() <= 0) return false;
+    return dev || h.getImageSizeBytes() > kHostBz2Bytes;
+}
+
 // the GPU bzip2 decoder (env LFM_GPU_BUNZIP2=0: host libbz2 per block)
 bool gpu_bunzip2_enabled()
 {
@@ -540,7 +553,7 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     // box), but its wall time is then mostly queueing (4-8 ms) and the
     // predictor after it runs 5-10 % slower (more dirty lines in the caches).
     static const bool early = std::getenv("LFM_PRESELECT_EARLY") && std::atoi(std::getenv("LFM_PRESELECT_EARLY")) == 1;
-    const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
+    const bool gpu_bz = use_gpu_bzip2(h, dev);
     const int req0 = h.headerVersion & 0x7F;
     int pre_k = -1;
     float pre_ent[8] = {0};
@@ -1563,7 +1576,7 @@ int Encoder::encode_set(const void* img, bool dev, klb_image_header& h, Sink& si
     if (int rc = normalize_header(h)) return rc;
     const uint8_t* sym = nullptr;
     const uint8_t* dsym = nullptr;
-    const bool gpu_bz = gpu_bzip2_enabled() && h.compressionType == BZIP2 && lfm_hip_device_count() > 0;
+    const bool gpu_bz = use_gpu_bzip2(h, dev);
     int rc = predictor_stage(img, dev, h, &sym, gpu_bz ? &dsym : nullptr, st, slab ? *slab : whole, set);
     if (rc) return rc;
     auto tc = clk::now();

@@ -470,7 +470,9 @@ def test_gpu_bzip2_host_fallback_streams(lfmlib, oracle, gpu):
     img = np.stack([runs4[:95000].reshape(1, 95000), np.tile(np.array([[3, 7]], np.uint8), (1, 47500))])
     img = img.reshape(1, 1, 2, 1, 95000)  # x = 95000, z = 2: two streams of one row each
     enc = lfmlib.Encoder(device=0)
-    b, st = enc.encode(img, header_version=8, nnum=13, block_size=[95000, 1, 1, 1, 1])
+    # device-resident (a host image this small goes to the host library whole)
+    b, st = enc.encode(torch.from_numpy(img.copy()).cuda(), header_version=8, nnum=13,
+                       block_size=[95000, 1, 1, 1, 1])
     enc.close()
     assert b == oracle.encode(img, header_version=8, nnum=13, data_type=0, block_size=[95000, 1, 1, 1, 1])
 
