@@ -47,7 +47,6 @@ constexpr int kMaxGroups = 6;
 constexpr int kMaxAlpha = 258;
 constexpr int kMaxSel = 18002;
 constexpr int kMaxLen = 20;
-constexpr int kLutBits = 10;
 constexpr uint32_t kMark = 128;  // cycle nodes per inverse-BWT walker (on average)
 constexpr uint32_t kWalkKeep = 512;  // bytes a walker keeps from its one walk (segments are
                                      // geometric, mean kMark: 1.8 % of them are longer)
@@ -80,7 +79,6 @@ struct Dec {
     uint32_t* flags;
     uint32_t* out_len;
     uint32_t sel_cap;         // selectors that fit the decoder's LDS
-    uint32_t dpp_scan;        // 1: output offsets by a DPP wave scan (LFM_BZD_DPP, default), 0: shuffles
 };
 
 // MSB-first bit reader over the payload: a 64-bit window of two big-endian
@@ -311,7 +309,6 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
     extern __shared__ uint32_t sel[];
     const uint32_t lane = threadIdx.x;
     const uint32_t s = blockIdx.x;
-    const bool dpp_scan = D.dpp_scan != 0;
     uint32_t flag = 0;
     WaveBits br;
     const uint64_t b0 = D.offs[s], b1 = D.offs[s + 1];
@@ -589,16 +586,7 @@ __global__ __launch_bounds__(64) void bzd_huff(Dec D)
             const uint32_t fb = (uint32_t)__shfl((int)outb, max(p, 0));
             const uint32_t b = isrun ? (p < 0 ? front0 : fb) : outb;
             // 3. offsets (exclusive prefix sum of the counts) and the stores
-            uint32_t incl;
-            if (dpp_scan) {
-                incl = wave_sum_incl(cnt);
-            } else {
-                incl = cnt;
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-                    if ((int)lane >= d) incl += o;
-                }
-            }
+            const uint32_t incl = wave_sum_incl(cnt);
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             if (nblock + total > cap) { flag = kHost; break; }
             const uint32_t at = nblock + incl - cnt;
@@ -1223,61 +1211,16 @@ extern "C" int lfm_hip_bunzip2_issue(const void* d_payload, const uint64_t* h_of
     if (hipMemcpyAsync(d_offs, h_offs, ((size_t)count + 1) * 8, hipMemcpyHostToDevice, st) != hipSuccess)
         return LFM_HIP_ERUNTIME;
     D.sel_cap = std::min<uint32_t>(kMaxSel, (D.cap + 49) / 50 + 64);
-    static const uint32_t dpp_env = [] {
-        const char* e = getenv("LFM_BZD_DPP");
-        return e ? (uint32_t)(atoi(e) != 0) : 1u;
-    }();
-    D.dpp_scan = dpp_env;
     const size_t sel_lds = ((D.sel_cap + 7) / 8 * 4 + 15) & ~(size_t)15;
-    static const int lut_bits = [] {
-        const char* e = getenv("LFM_BZD_LUT_BITS");
-        const int b = e ? atoi(e) : 8;
-        return b == 9 || b == 10 ? b : 8;
-    }();
-    // the symbol loop's bit reader in vector registers (LFM_BZD_VALU=0: wave-uniform scalar reader)
-    static const bool valu = !(getenv("LFM_BZD_VALU") && atoi(getenv("LFM_BZD_VALU")) == 0);
-    if (lut_bits == 10) {
-        if (valu) hipLaunchKernelGGL((bzd_huff<10, true>), dim3(count), dim3(64), sel_lds, st, D);
-        else hipLaunchKernelGGL((bzd_huff<10, false>), dim3(count), dim3(64), sel_lds, st, D);
-    } else if (lut_bits == 9) {
-        if (valu) hipLaunchKernelGGL((bzd_huff<9, true>), dim3(count), dim3(64), sel_lds, st, D);
-        else hipLaunchKernelGGL((bzd_huff<9, false>), dim3(count), dim3(64), sel_lds, st, D);
-    } else {
-        if (valu) hipLaunchKernelGGL((bzd_huff<8, true>), dim3(count), dim3(64), sel_lds, st, D);
-        else hipLaunchKernelGGL((bzd_huff<8, false>), dim3(count), dim3(64), sel_lds, st, D);
-    }
-    // LF mapping: LFM_TT_THREADS (256 / 512 / 1024 positions per tile) for A/B runs
-    static const int tt_nt = [] {
-        const char* e = getenv("LFM_TT_THREADS");
-        const int v = e ? atoi(e) : kTtThreads;
-        return v == 512 || v == 1024 ? v : 256;
-    }();
-    if (tt_nt == 1024) hipLaunchKernelGGL(bzd_tt<1024>, dim3(count), dim3(1024), 0, st, D);
-    else if (tt_nt == 512) hipLaunchKernelGGL(bzd_tt<512>, dim3(count), dim3(512), 0, st, D);
-    else hipLaunchKernelGGL(bzd_tt<256>, dim3(count), dim3(256), 0, st, D);
-    // inverse-BWT walk: LFM_WALK_THREADS (256 / 512 (default) / 1024 per stream) and
-    // LFM_WALK_LDSM (marker tables in LDS, default on) for A/B runs
-    static const int walk_nt = [] {
-        const char* e = getenv("LFM_WALK_THREADS");
-        const int v = e ? atoi(e) : 512;
-        return v == 256 || v == 1024 ? v : 512;
-    }();
-    static const bool walk_ldsm = [] {
-        const char* e = getenv("LFM_WALK_LDSM");
-        return e ? atoi(e) != 0 : true;
-    }();
-    // (large blocks, level 5 and up, keep the tables in global memory: LDS
-    // for ~2 workgroups per CU at most)
+    // (9- / 10-bit lookup tables and a wave-uniform scalar bit reader measured slower)
+    hipLaunchKernelGGL((bzd_huff<8, true>), dim3(count), dim3(64), sel_lds, st, D);
+    hipLaunchKernelGGL(bzd_tt<kTtThreads>, dim3(count), dim3(kTtThreads), 0, st, D);
+    // inverse-BWT walk, 512 threads per stream, the marker tables in LDS
+    // (large blocks, level 5 and up, keep them in global memory: LDS for ~2
+    // workgroups per CU at most)
     const size_t wl = (size_t)D.mcap * 16;
-    if (walk_ldsm && wl <= 48 * 1024) {
-        if (walk_nt == 1024) hipLaunchKernelGGL((bzd_walk<1024, true>), dim3(count), dim3(1024), wl, st, D);
-        else if (walk_nt == 512) hipLaunchKernelGGL((bzd_walk<512, true>), dim3(count), dim3(512), wl, st, D);
-        else hipLaunchKernelGGL((bzd_walk<256, true>), dim3(count), dim3(256), wl, st, D);
-    } else {
-        if (walk_nt == 1024) hipLaunchKernelGGL((bzd_walk<1024, false>), dim3(count), dim3(1024), 0, st, D);
-        else if (walk_nt == 512) hipLaunchKernelGGL((bzd_walk<512, false>), dim3(count), dim3(512), 0, st, D);
-        else hipLaunchKernelGGL((bzd_walk<256, false>), dim3(count), dim3(256), 0, st, D);
-    }
+    if (wl <= 48 * 1024) hipLaunchKernelGGL((bzd_walk<512, true>), dim3(count), dim3(512), wl, st, D);
+    else hipLaunchKernelGGL((bzd_walk<512, false>), dim3(count), dim3(512), 0, st, D);
     hipLaunchKernelGGL(bzd_rle1, dim3(count), dim3(64), 0, st, D);
     if (hipGetLastError() != hipSuccess) return LFM_HIP_ERUNTIME;
     if (hipMemcpyAsync(h_lens, D.out_len, (size_t)count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -524,10 +524,9 @@ constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 %
 // previous device-wide 60-bit radix sort made 8 HBM passes.  Chunks above the
 // large sorter's capacity (one bucket of > kBigCap equal-prefix rotations) go
 // to a rocPRIM segmented sort.
-constexpr uint32_t kBucketBits = 14;               // default: 64 KiB histogram, two workgroups per CU (LFM_BKT_BITS 13..15;
-                                                   // 15 bits / one workgroup per CU measured 3 % slower end to end,
-                                                   // 13 bits 18 % slower: more buckets overflow the small sorter)
-constexpr uint32_t kMinBucketBits = 13, kMaxBucketBits = 15;
+constexpr uint32_t kBucketBits = 14;               // 64 KiB histogram, two workgroups per CU (15 bits / one workgroup
+                                                   // per CU measured 3 % slower end to end, 13 bits 18 % slower: more
+                                                   // buckets overflow the small sorter)
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
 constexpr uint32_t kChunk = 1024;
@@ -2161,7 +2160,7 @@ __global__ __launch_bounds__(64) void huff_init(Batch B)
 // multiple of 4): no LDS tile, so ~8 KiB of LDS per workgroup and more
 // workgroups per CU to hide the loads.  The last, partial group pads with
 // symbol kMaxAlpha, whose packed lengths are 0 and which is not counted.
-// Same selectors and frequencies as huff_select (LFM_HSEL=0 selects that one).
+// (A 25 KiB LDS tile of the symbols measured 3.4x slower: fewer workgroups per CU.)
 __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
 {
     __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
@@ -2954,11 +2953,9 @@ size_t prim_tmp_bytes(uint32_t count, uint32_t cap)
     uint8_t* f = nullptr;
     size_t tmp = 0, q = 0;
     const size_t max_seg = (size_t)count * (cap / kBigCap + 1);
-    for (uint32_t bits = kMinBucketBits; bits <= kMaxBucketBits; ++bits) {
-        (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, (unsigned)max_seg, v, v, 0,
-                                                  64 - bits);
-        tmp = std::max(tmp, q);
-    }
+    (void)rocprim::segmented_radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, (unsigned)max_seg, v, v, 0,
+                                              64 - kBucketBits);
+    tmp = std::max(tmp, q);
     (void)rocprim::radix_sort_pairs(nullptr, q, k, k, v, v, (unsigned)N, 0, 64);
     tmp = std::max(tmp, q);
 

@@ -519,40 +519,17 @@ void Encoder::Inflight::wait_release()
     cv.wait(lk, [&] { return released; });
 }
 
-// release stage of the pipelined encodes (lfm_hip_bzip2_set_stage_hook stages)
-static int pipe_release_stage()
-{
-    static const int v = [] {
-        const char* e = std::getenv("LFM_PIPE_AT");
-        const int x = e ? std::atoi(e) : 0;
-        return x >= 0 && x <= 2 ? x : 0;
-    }();
-    return v;
-}
-
 int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads, const SlabSpec* slab,
                     uint64_t* ticket)
 {
-    static const bool trace = std::getenv("LFM_TRACE_SUBMIT") && std::atoi(std::getenv("LFM_TRACE_SUBMIT")) != 0;
-    auto ts = [](const char* what) {
-        std::fprintf(stderr, "[submit %.3f] %s\n",
-                     std::chrono::duration<double, std::milli>(clk::now().time_since_epoch()).count(), what);
-    };
-    if (trace) ts("enter");
     static const SlabSpec whole;
     if (threads <= 0) threads = default_threads();
     const int p = par_;
     Inflight& f = fly_[p];
     if (f.th.joinable()) f.th.join();  // the encode before last used this buffer set
-    // Auto-selection (klb_imageIO.cpp:2316-2360) on the encoder's stream, once
-    // the previous encode's kernels are done (its release); the request then
-    // becomes the forced 8 + k (video bit kept) for the predictor stage, the
-    // bytes are the same.  LFM_PRESELECT_EARLY=1 runs it before that wait
-    // instead, interleaved with the previous encode's GPU bzip2: same
-    // throughput within noise (10 966-11 361 vs 11 046-11 047 Mpixel/s, same
-    // box), but its wall time is then mostly queueing (4-8 ms) and the
-    // predictor after it runs 5-10 % slower (more dirty lines in the caches).
-    static const bool early = std::getenv("LFM_PRESELECT_EARLY") && std::atoi(std::getenv("LFM_PRESELECT_EARLY")) == 1;
+    // Auto-selection (klb_imageIO.cpp:2316-2360) on the encoder's stream; the
+    // request then becomes the forced 8 + k (video bit kept) for the
+    // predictor stage, the bytes are the same.
     const bool gpu_bz = use_gpu_bzip2(h, dev);
     const int req0 = h.headerVersion & 0x7F;
     int pre_k = -1;
@@ -563,21 +540,18 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         if (int rc = preselect(img, dev, h, slab ? *slab : whole, &pre_k, pre_ent)) return rc;
         pre_ms = ms_since(ts0);
         h.headerVersion = (uint8_t)((h.headerVersion & 0x80) | (8 + pre_k));
-        if (trace) ts("selected");
         return 0;
     };
     const bool pre = gpu_bz && req0 < NUM_PREDICTORS && h.getBytesPerPixel() == 2 && h.Nnum > 0;
     // a host stack starts its chunked upload (and the predictor on the chunks
     // that have landed) before the previous encode is released: the PCIe
-    // upload runs under the previous encode's GPU bzip2
-    // a device stack, too, runs its selection and predictor stage before that
-    // wait, beside the previous encode's tail (its own buffer set; the
-    // selection then queues behind that tail, ~12 ms of host wall time, and the
-    // predictor kernel shares the CUs): config 3 pipelined 12 068-12 158 vs
-    // 11 797-11 872 Mpixel/s, same box (profiles/r04_ab_predict_early.txt);
-    // LFM_PREDICT_EARLY=0 waits for the release first
-    static const bool predict_early = env_int("LFM_PREDICT_EARLY", 1) == 1;
-    const bool host_early = gpu_bz && (upload_pipe_ok(dev, h) || (predict_early && dev));
+    // upload runs under the previous encode's GPU bzip2.  A device stack, too,
+    // runs its selection and predictor stage before that wait, beside the
+    // previous encode's tail (its own buffer set; the selection then queues
+    // behind that tail and the predictor kernel shares the CUs): config 3
+    // pipelined 12 068-12 158 vs 11 797-11 872 Mpixel/s waiting for the
+    // release first, same box (profiles/r04_ab_predict_early.txt)
+    const bool host_early = gpu_bz && (upload_pipe_ok(dev, h) || dev);
     f.ticket = next_ticket_++;
     f.rc = 0;
     std::memset(&f.st, 0, sizeof(f.st));
@@ -595,7 +569,7 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         f.release();
         return rc;
     };
-    if (pre && (early || host_early))
+    if (pre && host_early)
         if (int rc = select_now()) return fail(rc);
     if (pre_k >= 0) {
         f.st.select_ms = pre_ms;
@@ -616,8 +590,7 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         if (int rc = predictor_stage(img, dev, h, nullptr, &dsym, &f.st, slab ? *slab : whole, p)) return fail(rc);
     }
     fly_[p ^ 1].wait_release();        // the previous encode is in its tail
-    if (trace) ts("released");
-    if (pre && !early && !host_early) {
+    if (pre && !host_early) {
         if (int rc = select_now()) return fail(rc);
         f.st.select_ms = pre_ms;
         std::memcpy(f.st.entropy, pre_ent, sizeof(pre_ent));
@@ -646,7 +619,6 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         }
         dsym = (const uint8_t*)d_sym_[p];
     }
-    if (trace) ts("predicted");
     auto hh = std::make_shared<klb_image_header>(h);
     f.th = std::thread([this, &f, hh, dsym, level, p, t0]() {
         (void)hipSetDevice(device_);
@@ -697,16 +669,9 @@ int Encoder::ensure_gpu()
         if (hipGetDevice(&device_) != hipSuccess) device_ = 0;
     }
     if (device_ >= n || hipSetDevice(device_) != hipSuccess) return kErrNoGpu;
-    // the predictor stage (selection + fused predictor) can run at the device's
-    // highest stream priority, so a pipelined submit's short kernels go ahead
-    // of the previous encode's GPU bzip2 work still queued on the other streams
-    // (env LFM_PRED_PRIO=1; off by default: measured slower end to end)
-    static const bool prio = std::getenv("LFM_PRED_PRIO") && std::atoi(std::getenv("LFM_PRED_PRIO")) == 1;
-    int prio_lo = 0, prio_hi = 0;
-    if (!prio || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_hi) != hipSuccess) {
-        if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
-    }
+    // the predictor stage's stream (a high-priority one measured 10 % slower
+    // end to end: it took a hardware queue from the bzip2 slots)
+    if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return kErrNoGpu;
     // the first buffer set's GPU bzip2 slot streams are created right after
     // the predictor stream, so each lands on a hardware queue of its own
     // (GPU_MAX_HW_QUEUES is 4, the null stream holding one): streams created
@@ -1253,15 +1218,11 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         return (size_t)(v > 0 ? v : 48 * 1024) << 20;
     }();
     const size_t per_stream = lfm_hip_bzip2_workspace_bytes(1, block_bytes) + out_cap;
-    // batches per slot (env LFM_BZ2_BATCHES_PER_SLOT, default 1): more, smaller
-    // batches let the in-order writer's copies overlap later batches' kernels
-    static const uint64_t per_slot = [] {
-        const char* e = std::getenv("LFM_BZ2_BATCHES_PER_SLOT");
-        const long v = e ? std::atol(e) : 0;
-        return (uint64_t)(v > 0 ? v : 1);
-    }();
+    // one batch per slot (smaller batches, so the in-order writer's copies
+    // overlap later batches' kernels, measured slower: the latency-bound
+    // stages cost per batch)
     const int slots = bz_slot_count();
-    const uint64_t nway = slots * per_slot;
+    const uint64_t nway = slots;
     uint64_t batch = std::max<uint64_t>(1, std::min<uint64_t>((nblocks + nway - 1) / nway,
                                                                 budget / slots / per_stream));
     batch = std::min<uint64_t>(batch, ((1ull << 32) - 1) / rle_cap);
@@ -1302,39 +1263,11 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
     std::vector<std::array<double, 5>> stage_ms(nslots);  // per slot, summed over its batches
     for (auto& a : stage_ms) a.fill(0.0);
     // pipelined encodes: the next submit starts once every batch of the last
-    // round has passed the release stage (hook of lfm_hip_bzip2_blocks)
-    const int release_at = pipe_release_stage();
-    // LFM_BZ2_STAGGER=1 / 2 (experiment): slot 1 starts its first batch once
-    // slot 0's first batch has passed its BWT / MTF stage, so the slots'
-    // latency-bound stages (MTF, Huffman tables) run beside the other slot's
-    // sorts instead of in lockstep
-    static const int stagger = [] {
-        const char* e = std::getenv("LFM_BZ2_STAGGER");
-        const int v = e ? std::atoi(e) : 0;
-        return v == 1 || v == 2 ? v : 0;
-    }();
-    struct HookCtx {
-        Inflight* fly;
-        int stage;       // release stage for the pipelined encodes (fly)
-        int stagger;     // stage that lets slot 1 start (0: none)
-        std::mutex* mu;
-        std::condition_variable* cv;
-        bool* go;        // slot 1 may start
-    };
-    bool stagger_go = !stagger || nslots < 2;
-    HookCtx hctx{fly, release_at, 0, &mu, &cv, &stagger_go};
-    HookCtx sctx{fly, release_at, stagger, &mu, &cv, &stagger_go};
-    auto hook = [](void* ctx, int stage) {
-        HookCtx* c = (HookCtx*)ctx;
-        if (c->fly && c->stage > 0 && stage == c->stage) c->fly->reach();
-        if (c->stagger && stage == c->stagger) {
-            {
-                std::lock_guard<std::mutex> lk(*c->mu);
-                *c->go = true;
-            }
-            c->cv->notify_all();
-        }
-    };
+    // round has run its kernels (releasing it after the BWT or the MTF of
+    // those batches measured equal or slower: the next stack's kernels slow
+    // this one's latency-bound Huffman chains as much as they gain; staggering
+    // the two slots measured slower too, their latency-bound stages overlap
+    // each other in lockstep)
     // host stack still uploading (start_upload): a batch waits for the chunks
     // holding its last block (blocks run x -> y -> z -> c -> t, so that block
     // reaches furthest into the flattened (t, c, z) frame order)
@@ -1356,13 +1289,6 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
         (void)hipSetDevice(device_);
         BzSlot& sl = bz_[k];
         for (uint64_t b = k; b < nbatch; b += nslots) {
-            const bool rel_hook = fly && release_at > 0 && b + nslots >= nbatch;
-            const bool stg_hook = !stagger_go && b == 0;  // slot 0's first batch lets slot 1 go
-            if (rel_hook || stg_hook) lfm_hip_bzip2_set_stage_hook(hook, stg_hook ? (void*)&sctx : (void*)&hctx);
-            if (k == 1 && b == 1) {  // slot 1's first batch waits for the stagger point
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stagger_go || abort_all.load(); });
-            }
             if (b >= (uint64_t)nslots) {  // wait until the writer consumed batch b - nslots
                 std::unique_lock<std::mutex> lk(mu);
                 cv.wait(lk, [&] { return state[b - nslots] != 1 || abort_all.load(); });
@@ -1380,15 +1306,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
             }
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
                                           ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
-            if (fly && b + nslots >= nbatch && release_at == 0) fly->reach();
-            if (rel_hook || stg_hook) lfm_hip_bzip2_set_stage_hook(nullptr, nullptr);
-            if (stg_hook) {  // (also when the batch never reached the stage)
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    stagger_go = true;
-                }
-                cv.notify_all();
-            }
+            if (fly && b + nslots >= nbatch) fly->reach();
             float sm[5];
             if (ok && lfm_hip_bzip2_last_stage_ms(sm) == 0)
                 for (int i = 0; i < 5; ++i) stage_ms[k][i] += sm[i];
@@ -2070,11 +1988,6 @@ bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int th
         if (i + 2 < nc && !issue(i + 2)) return false;
     }
     return true;
-}
-
-bool staged_d2h(void* h_dst, const void* d_src, size_t n, hipStream_t st, int threads)
-{
-    return staged_d2h(h_dst, d_src, n, st, threads, staging());
 }
 
 // Device buffers, streams and pinned status arrays of the GPU decode, kept

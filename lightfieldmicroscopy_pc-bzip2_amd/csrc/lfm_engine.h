@@ -150,13 +150,12 @@ public:
     // sets (symbols, bzip2 slots and workspaces, pinned output) used in turn:
     // submit runs the predictor stage of its stack into one set and hands the
     // GPU bzip2 + in-order assembly + payload copies to a finisher thread.
-    // The next submit starts once the previous encode's batches have passed
-    // the release stage (env LFM_PIPE_AT: 0 = when its kernels are done, the
-    // default, so the next stack's kernels overlap its assembly and payload
-    // copies; 1 = after its BWT, 2 = after its MTF, so they also overlap its
-    // latency-bound tail -- measured 8 943 / 9 035 vs 9 098 Mpixel/s: the
-    // heap chains slow down as much as the head gains).  At most two encodes
-    // are in flight.  The input may be released when submit returns (the
+    // The next submit's GPU bzip2 starts once the previous encode's kernels
+    // are done, so the next stack's kernels overlap its assembly and payload
+    // copies (releasing it after its BWT or its MTF, so they also overlap its
+    // latency-bound tail, measured 8 943 / 9 035 vs 9 098 Mpixel/s: the heap
+    // chains slow down as much as the head gains).  At most two encodes are
+    // in flight.  The input may be released when submit returns (the
     // predictor stage has consumed it).
     int submit(const void* img, bool dev, klb_image_header& h, int threads, const SlabSpec* slab, uint64_t* ticket);
     // wait for a submitted encode: its .lfm is *out (valid until the second

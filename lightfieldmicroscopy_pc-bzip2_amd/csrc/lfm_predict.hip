@@ -1268,15 +1268,6 @@ struct VecShape {
     static constexpr int PD = 3;
 };
 
-static bool vec_enabled()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("LFM_PRED_VEC");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-}
-
 template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
 static hipError_t launch_vec_shape(const FrameSet& p, hipStream_t st)
 {
@@ -1340,21 +1331,12 @@ static hipError_t launch_vec_pairs(const FrameSet& p, hipStream_t st)
     return hipSuccess;
 }
 
-static bool pairs_enabled()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("LFM_PRED_PAIRS");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-}
-
 template <int FAM, int K>
 static hipError_t launch_vec(const FrameSet& p, hipStream_t st)
 {
     using S = VecShape<FAM>;
     using PS = PairShape<FAM>;
-    const bool pairs = p.video && p.nz >= 2 && pairs_enabled();
+    const bool pairs = p.video && p.nz >= 2;
     if (p.T == 15) {
         if (pairs) return launch_vec_pairs<FAM, K, 15, PS::WPR, PS::NCW, PS::RPW, PS::PD>(p, st);
         return launch_vec_shape<FAM, K, 15, S::WPR, S::NCW, S::RPW, S::PD>(p, st);
@@ -1365,7 +1347,7 @@ static hipError_t launch_vec(const FrameSet& p, hipStream_t st)
 
 static bool vec_ok(const FrameSet& p, int force_generic)
 {
-    return !force_generic && vec_enabled() && (p.T == 13 || p.T == 15) && (p.W % 8) == 0 && p.W >= 32;
+    return !force_generic && (p.T == 13 || p.T == 15) && (p.W % 8) == 0 && p.W >= 32;
 }
 
 template <int FAM, int K>

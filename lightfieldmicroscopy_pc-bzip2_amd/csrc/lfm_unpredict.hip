@@ -71,9 +71,6 @@ struct UnFrames {
     uint16_t* out;         // nz decoded frames
     int W, H, T, nz, z0, video;
     int first, step;       // this launch decodes local frames first, first + step, ...
-    // diagnostics (LFM_UNPREDICT_TRACE): per band5 workgroup, kTraceSlots
-    // 100 MHz timestamps (band start, then before / after each round's wait)
-    unsigned long long* trace;
     // band4 / band5 hand-over: a wait gives up after spin_limit polls (a
     // band that never sees its producer must not hang the device) and then
     // sets *err (band5: global memory, checked by the launcher, which re-runs
@@ -81,7 +78,6 @@ struct UnFrames {
     int spin_limit;
     int* err;
 };
-constexpr int kTraceSlots = 512;
 constexpr int kSpinLimit = 1 << 24;  // ~0.45 s of s_sleep 1 polls
 
 template <int FAM, int K>
@@ -554,18 +550,9 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
         nf.v[NB_A] = 0;
         load_far(nf, -r);
         const int edge_k = T + 63;  // before this step some lane has x < T
-        unsigned long long* tr = nullptr;
-        if constexpr (XCU) {
-            if (p.trace) {
-                tr = p.trace + (size_t)blockIdx.x * kTraceSlots;
-                if (r == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
-            }
-        }
         // the last round (k0 = W + 64) only stores every row's last group
         for (int ks = 0; ks < W + 72; ks += kSync) {
             {
-                const int rd = ks / kSync;
-                if (tr && r == 0 && 2 + 2 * rd < kTraceSlots) tr[1 + 2 * rd] = __builtin_amdgcn_s_memrealtime();
                 // every store issued before the last round has completed: the
                 // pixels of steps < ks - 24 are in memory (a pixel of step s is
                 // stored by the round starting at <= s + 15)
@@ -581,7 +568,6 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
                     wait_ge((b - 1) * stride + min(ks + 2 * kSync + 72, kend));
                     hload(ks + kSync);
                 }
-                if (tr && r == 0 && 2 + 2 * rd < kTraceSlots) tr[2 + 2 * rd] = __builtin_amdgcn_s_memrealtime();
             }
 #pragma unroll
             for (int q = 0; q < kSync / 8; ++q) {
@@ -649,7 +635,6 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
             __builtin_amdgcn_s_waitcnt(0);
         }
         if (r == 0) __hip_atomic_store(pos + wv, b * stride + kend, __ATOMIC_RELAXED, kScope);
-        if (tr && r == 0) tr[kTraceSlots - 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -716,7 +701,7 @@ static size_t band2_lds(const UnFrames& p) { return (size_t)(64 * kRing + (p.T +
 
 static bool band2_ok(const UnFrames& p)
 {
-    return p.T <= 30 && band2_lds(p) <= 160 * 1024 && !std::getenv("LFM_UNPREDICT_V1");
+    return p.T <= 30 && band2_lds(p) <= 160 * 1024;
 }
 
 // waves per frame for band4 (0: not applicable; rows are read and written in
@@ -724,25 +709,9 @@ static bool band2_ok(const UnFrames& p)
 static int band4_waves(const UnFrames& p)
 {
     // (band4 / band5 address a frame through 31-bit buffer offsets)
-    if (p.T < 2 || p.T > 30 || (p.W & 7) || (size_t)p.W * p.H * 2 >= 0x7FFFFFF0u || std::getenv("LFM_UNPREDICT_V3") ||
-        std::getenv("LFM_UNPREDICT_V2"))
-        return 0;
-    static const int cap = [] {
-        const char* e = std::getenv("LFM_UNPREDICT_NW");
-        return e ? std::max(2, std::min(8, std::atoi(e))) : 8;
-    }();
-    const int nw = std::min(cap, (p.H + 63) / 64);
+    if (p.T < 2 || p.T > 30 || (p.W & 7) || (size_t)p.W * p.H * 2 >= 0x7FFFFFF0u) return 0;
+    const int nw = std::min(8, (p.H + 63) / 64);
     return nw >= 2 ? nw : 0;
-}
-
-// band5 unless LFM_UNPREDICT_XCU=0 (band4 then keeps a frame's bands on one CU)
-static bool band5_enabled()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("LFM_UNPREDICT_XCU");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
 }
 
 // hand-over poll limit: kSpinLimit, or LFM_UNPREDICT_SPIN (tests force a
@@ -757,7 +726,7 @@ static int spin_limit()
 template <int FAM, int K_>
 static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool no_band5 = false)
 {
-    if (band4_waves(p) && band5_enabled() && !no_band5) {
+    if (band4_waves(p) && !no_band5) {
         const int nbands = (p.H + 63) / 64;
         const size_t lds = (size_t)(64 * kRing + (p.T + 1) * kHand) * 2;
         int* pos = nullptr;
@@ -766,13 +735,9 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool
         if (hipMallocAsync((void**)&pos, pbytes + sizeof(int), st) != hipSuccess) return hipErrorOutOfMemory;
         hipError_t e = hipMemsetAsync(pos, 0xFF, pbytes, st);  // -1: no progress yet
         if (e == hipSuccess) e = hipMemsetAsync(pos + (size_t)grid * nbands, 0, sizeof(int), st);
-        static const char* trace_path = std::getenv("LFM_UNPREDICT_TRACE");
         UnFrames pt = p;
         pt.spin_limit = spin_limit();
         pt.err = pos + (size_t)grid * nbands;
-        const size_t tbytes = (size_t)grid * nbands * kTraceSlots * sizeof(unsigned long long);
-        if (trace_path && e == hipSuccess && hipMalloc((void**)&pt.trace, tbytes) == hipSuccess)
-            e = hipMemsetAsync(pt.trace, 0, tbytes, st);
         if (e == hipSuccess) {
             hipLaunchKernelGGL((unpredict_band5<FAM, K_>), dim3(grid * nbands), dim3(64), lds, st, pt, pos, nbands,
                                grid);
@@ -796,18 +761,6 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool
             if (!fallback) e = hipErrorLaunchTimeOut;
             else e = launch_band2<FAM, K_>(p, grid, st, true);
         }
-        if (pt.trace) {  // diagnostics: [int32 nfr, int32 nbands, int32 slots][u64 per slot]
-            std::vector<unsigned long long> h(tbytes / sizeof(unsigned long long));
-            if (e == hipSuccess) e = hipMemcpyAsync(h.data(), pt.trace, tbytes, hipMemcpyDeviceToHost, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            (void)hipFree(pt.trace);
-            if (FILE* f = e == hipSuccess ? std::fopen(trace_path, "ab") : nullptr) {
-                const int hd[3] = {grid, nbands, kTraceSlots};
-                std::fwrite(hd, sizeof(hd), 1, f);
-                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
-                std::fclose(f);
-            }
-        }
         return e;
     }
     if (const int nw = band4_waves(p)) {
@@ -820,8 +773,7 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool
     }
     const size_t lds = band2_lds(p);
     // band3 reads a step's far neighbours one step early: T >= 2
-    static const bool v2_env = std::getenv("LFM_UNPREDICT_V2") != nullptr;
-    const bool v2 = v2_env || p.T < 2;
+    const bool v2 = p.T < 2;
     const void* fn = v2 ? (const void*)unpredict_band2<FAM, K_> : (const void*)unpredict_band3<FAM, K_>;
     if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return hipErrorInvalidValue;
@@ -872,7 +824,7 @@ extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, 
     const bool any_temporal = video && (nframes > 1 || (z0 & 1));
     if (any_temporal && family != 0) return LFM_HIP_ENOTINV;  // ((I - pred) + P) >> 1 drops a bit
     if (video && (z0 & 1) && !d_prev) return LFM_HIP_EINVAL;
-    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, nullptr, lfm::kSpinLimit, nullptr};
+    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, lfm::kSpinLimit, nullptr};
     // without video every frame is spatial: one launch; with video the
     // spatial (even global z) frames first, then the temporal ones on their
     // decoded predecessors

@@ -789,12 +789,10 @@ def test_submit_select_frame_and_wait_codes(lfmlib, oracle, gpu):
         lfmlib.set_family("tiles")
 
 
-@pytest.mark.parametrize("env", ["LFM_DECODE_H2D=1", "LFM_DECODE_H2D=2",
-                                 "LFM_WALK_LDSM=0 LFM_WALK_THREADS=256", "LFM_WALK_THREADS=1024 LFM_TT_THREADS=1024"])
+@pytest.mark.parametrize("env", ["LFM_DECODE_H2D=1", "LFM_DECODE_H2D=2"])
 def test_decode_path_switches(lfmlib, oracle, gpu, tmp_path, env):
-    """The decode's alternative paths (payload upload by one runtime copy or
-    by hipMemcpyAsync from the pinned chunks instead of the SDMA engine; walk
-    marker tables in global memory, other walk / LF-mapping widths) restore
+    """The decode's fallback payload uploads (one runtime copy, or
+    hipMemcpyAsync from the pinned chunks, instead of the SDMA engine) restore
     the same pixels.  The switches are read once per process: each variant
     decodes in its own child process (one GPU process at a time)."""
     import subprocess

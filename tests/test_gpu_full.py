@@ -108,6 +108,32 @@ def test_config5_volume_roundtrip(lfmlib, gpu):
     assert np.array_equal(out.reshape(d.shape), d.cpu().numpy().view(np.uint16))
 
 
+@pytest.mark.parametrize("t", [50, 99])
+def test_config5_far_volume(lfmlib, gpu, t):
+    """t-volume 50 / 99 of the 100-volume config-5 stack (4096 x 4096 x 32,
+    video, tiles): coded alone with the predictor chosen on volume 0's frame 0
+    (request 8 + k, video bit) its block streams equal the oracle's per-volume
+    digest (cfg5far), and the GPU decode returns every pixel."""
+    e = _full("cfg5far_4096x4096x32x1x100_video_tiles_auto")
+    X, Y, Z = e["xyzct"][:3]
+    want = e["volumes"][str(t)]
+    torch = gpu
+    d = torch.empty((Z, Y, X), dtype=torch.int16, device="cuda")
+    lfmlib.synth_device(d, X, Y, Z, e["nnum"], t_index=t, idx0=t * Z * X * Y, seed=e["seed"])
+    lfmlib.set_family("tiles")
+    enc = lfmlib.Encoder(device=0)
+    try:
+        buf, st = enc.encode(d, header_version=0x80 | (8 + e["chosen"]), nnum=e["nnum"])
+        assert st["header_version"] == e["final_header_version"]
+    finally:
+        enc.close()
+    base = 320 + 8 * e["nblocks_per_volume"]
+    assert len(buf) - base == want["bytes"]
+    assert hashlib.sha256(bytes(buf[base:])).hexdigest() == want["sha256"]
+    out = lfmlib.decode(buf)
+    assert np.array_equal(out.reshape(d.shape), d.cpu().numpy().view(np.uint16))
+
+
 _CFG5X4_CHILD = r"""
 import hashlib, json, os, sys, time
 import numpy as np
