@@ -75,8 +75,8 @@ LFM_API int lfm_encoder_encode(lfm_encoder* enc, const void* img, int img_is_dev
  * with the stack's frame 0, or a forced request 8 + k.  Runs the predictor stage (img may
  * be released on return), then hands the GPU bzip2 stage, the .lfm assembly
  * and its payload copies (system DMA engine) to a finisher thread and
- * returns.  The next submit's GPU work starts once this encode's kernels are
- * done (env LFM_PIPE_AT: 1 / 2 start it after the BWT / MTF instead).  At
+ * returns.  The next submit's GPU bzip2 starts once this encode's kernels are
+ * done (its selection and predictor stage run before, beside this one).  At
  * most two encodes are in flight: a submit first joins the one before last.
  * *ticket names the encode for lfm_encoder_wait; errors of the finisher are
  * returned by lfm_encoder_wait. */
