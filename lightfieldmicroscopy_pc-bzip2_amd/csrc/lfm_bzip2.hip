@@ -53,6 +53,10 @@
 #include <vector>
 #include "lfm_hip.h"
 
+#ifndef LFM_IND_PROF
+#define LFM_IND_PROF 0  // bwt_induce phase clocks by printf (timing variants only; 0 in the library)
+#endif
+
 namespace lfm {
 namespace bz {
 
@@ -1378,7 +1382,7 @@ __global__ __launch_bounds__(256) void bwt_flag_periodic(Batch B, const uint32_t
 constexpr uint32_t kIndPend = 0xFFFFFFFFu;  // never an entry: nprev <= 3
 constexpr uint32_t kIndIdx = 0xFFFFFu;      // n < nblock_max < 2^20
 constexpr uint32_t kIndPlaced = 1u << 23;
-constexpr int kPlaceUnroll = 8;  // sorted slots per thread in flight (bwt_place_sorted)
+constexpr uint32_t kPlaceChunk = 2048;  // sorted slots / positions per bwt_place_sorted workgroup
 
 // q-order starts of each bucket (q0[c]), its placed part (p0[c], p1[c]) and
 // the first sa slot of its sorted rotations (s0[c]), 256 threads
@@ -1414,56 +1418,68 @@ __device__ __forceinline__ void ind_tables(const Batch& B, uint32_t s, uint32_t 
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void bwt_place_sorted(Batch B)
+// One workgroup per kPlaceChunk sorted slots and final positions of a
+// stream, the chunks of a stream consecutive on one XCD (workgroup w runs on
+// XCD w % 8): the text reads are random inside the stream, so a stream's text
+// should stay in one L2 while its chunks run.
+__global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks)
 {
     __shared__ uint32_t q0[256], p0[256], p1[256], s0[256], wtmp[8];
-    const uint32_t s = blockIdx.x, t = threadIdx.x;
-    if (B.flags[s] & kFlagHost) return;
+    const uint32_t t = threadIdx.x, k = blockIdx.x >> 3;
+    const uint32_t s = (blockIdx.x & 7u) + 8u * (k / chunks), base = (k % chunks) * kPlaceChunk;
+    if (s >= B.nstreams || (B.flags[s] & kFlagHost)) return;
     const uint32_t n = B.n[s], ns = B.nsub[s], mode = B.bwt_mode[s];
-    if (n == 0) return;
+    if (base >= n) return;
     ind_tables(B, s, mode, q0, p0, p1, s0, wtmp);
     const size_t o = (size_t)s * B.cap;
     const uint8_t* T = B.T + o;
     uint32_t* SF = B.sfin + o;
     uint32_t* SH = B.sfhi + o;
-    // the sorted slots, kPlaceUnroll per thread in flight: sa, then T[i-4 .. i]
-    constexpr int K = kPlaceUnroll;
-    for (uint32_t j0 = 0; j0 < ns; j0 += K * 256) {
-        uint32_t v[K], w0[K], w1[K];
+    // the sorted slots [base, base + kPlaceChunk): sa, then T[i-4 .. i], all
+    // loads issued before any is used
+    constexpr int K = kPlaceChunk / 256;
+    uint32_t v[K], w0[K], w1[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) v[k] = B.sa[o + min(j0 + k * 256 + t, ns - 1)];
+    for (int q = 0; q < K; ++q) v[q] = B.sa[o + min(base + q * 256 + t, ns ? ns - 1 : 0u)];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {  // two aligned dwords (clamped; the first four rotations wrap)
-            const uint32_t i = v[k] & kIdxMask, a = i >= 4 ? i - 4 : 0u;
-            const uint32_t* w = (const uint32_t*)(T + (a & ~3u));
-            w0[k] = w[0];
-            w1[k] = w[1];
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t j = j0 + k * 256 + t;
-            if (j >= ns) break;
-            const uint32_t i = v[k] & kIdxMask;
-            uint32_t x;  // T[i-4] | T[i-3] << 8 | T[i-2] << 16 | T[i-1] << 24
-            uint32_t c;  // T[i]
-            if (i >= 4) {
-                const uint32_t sh = ((i - 4) & 3u) * 8u;
-                const uint64_t d = (uint64_t)w0[k] | ((uint64_t)w1[k] << 32);
-                x = (uint32_t)(d >> sh);
-                c = (uint32_t)(d >> (sh + 32)) & 0xFFu;
-            } else {
-                x = 0;
-                for (uint32_t q = 1; q <= 4; ++q) x |= (uint32_t)T[(i + 4 * n - q) % n] << (32 - 8 * q);
-                c = T[i];
-            }
-            const uint32_t q = (mode == kModeSortA ? q0[c] : p1[c]) + (j - s0[c]);
-            SF[q] = mode == kModeFull ? v[k] : (v[k] | (3u << 20));
-            SH[q] = ((x >> 16) & 0xFFu) | (((x >> 8) & 0xFFu) << 8) | ((x & 0xFFu) << 16) | (c << 24);
-        }
+    for (int q = 0; q < K; ++q) {  // two aligned dwords (clamped; the first four rotations wrap)
+        const uint32_t i = v[q] & kIdxMask, a = i >= 4 ? i - 4 : 0u;
+        const uint32_t* w = (const uint32_t*)(T + (a & ~3u));
+        w0[q] = w[0];
+        w1[q] = w[1];
     }
-    // the positions still to place
-    for (uint32_t c = 0; c < 256; ++c)
-        for (uint32_t q = p0[c] + t; q < p1[c]; q += 256) SF[q] = kIndPend;
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        const uint32_t j = base + q * 256 + t;
+        if (j >= ns) break;
+        const uint32_t i = v[q] & kIdxMask;
+        uint32_t x;  // T[i-4] | T[i-3] << 8 | T[i-2] << 16 | T[i-1] << 24
+        uint32_t c;  // T[i]
+        if (i >= 4) {
+            const uint32_t sh = ((i - 4) & 3u) * 8u;
+            const uint64_t d = (uint64_t)w0[q] | ((uint64_t)w1[q] << 32);
+            x = (uint32_t)(d >> sh);
+            c = (uint32_t)(d >> (sh + 32)) & 0xFFu;
+        } else {
+            x = 0;
+            for (uint32_t r = 1; r <= 4; ++r) x |= (uint32_t)T[(i + 4 * n - r) % n] << (32 - 8 * r);
+            c = T[i];
+        }
+        const uint32_t qq = (mode == kModeSortA ? q0[c] : p1[c]) + (j - s0[c]);
+        SF[qq] = mode == kModeFull ? v[q] : (v[q] | (3u << 20));
+        SH[qq] = ((x >> 16) & 0xFFu) | (((x >> 8) & 0xFFu) << 8) | ((x & 0xFFu) << 16) | (c << 24);
+    }
+    // the positions [base, base + kPlaceChunk) still to place: the buckets
+    // overlapping the range, from the last one starting at or before base
+    const uint32_t end = min(n, base + kPlaceChunk);
+    uint32_t lo = 0, hi = 255;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (q0[mid] <= base) lo = mid;
+        else hi = mid - 1;
+    }
+    for (uint32_t c = lo; c < 256 && q0[c] < end; ++c)
+        for (uint32_t q = max(p0[c], base) + t; q < min(p1[c], end); q += 256) SF[q] = kIndPend;
 }
 
 // bwt_induce: one wave per stream scans in scan order, in blocks of
@@ -1478,6 +1494,7 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B)
 // of the same slice: the slice then runs in rounds up to its first pending lane.
 constexpr uint32_t kIndSlices = 8;
 constexpr uint32_t kIndBlock = 64 * kIndSlices;
+constexpr int kIndStepSlices = 4;  // slices scanned together (one round of ballots and LDS latencies)
 constexpr uint32_t kIndRing = 2 * kIndBlock;
 
 // LDS-DMA of one dword per lane into LDS at `lds` + 4 * lane, from L2 (sc1:
@@ -1553,83 +1570,161 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
     __syncthreads();
     issue(0);
     stage(0);
+#if LFM_IND_PROF
+    unsigned long long pt0 = 0, pt_issue = 0, pt_steps = 0, pt_stage = 0, pt_total = clock64();
+#define IND_T(x) do { const unsigned long long t_ = clock64(); x += t_ - pt0; pt0 = t_; } while (0)
+#else
+#define IND_T(x) do { } while (0)
+#endif
     bool bad = false;  // inconsistent counts or a pending entry no earlier lane places (never)
     for (uint32_t v0 = 0; v0 < n && !bad; v0 += kIndBlock) {
+#if LFM_IND_PROF
+        pt0 = clock64();
+#endif
         // the next block's ring slots held the previous block: not placed yet
 #pragma unroll
         for (uint32_t k = 0; k < kIndSlices; ++k) ring[(v0 + kIndBlock + 64 * k + lane) % kIndRing].x = kIndPend;
         const bool more = v0 + kIndBlock < n;
         if (more) issue(v0 + kIndBlock);
+        IND_T(pt_issue);
+        // steps of kIndStepSlices slices: item k of lane l is position
+        // vs + 64 k + l, and the scan order is (k, l)
+        for (uint32_t vs = v0; vs < min(n, v0 + kIndBlock) && !bad; vs += 64 * kIndStepSlices) {
+            constexpr int KS = kIndStepSlices;
+            uint2 e[KS];
+            bool valid[KS];
+            uint64_t todo[KS];
 #pragma unroll
-        for (uint32_t k = 0; k < kIndSlices; ++k) {
-            const uint32_t v = v0 + 64 * k + lane;
-            const bool valid = v < n;
-            uint64_t todo = __ballot(valid);
-            if (!todo) break;
-            const uint32_t r = v % kIndRing;
-            uint2 e = ring[r];
-            uint64_t pend = __ballot(valid && e.x == kIndPend);
-            // rounds over the lanes before the first pending one (one round
-            // unless an entry of the slice is placed by an earlier lane)
+            for (int k = 0; k < KS; ++k) {
+                const uint32_t v = vs + 64 * k + lane;
+                valid[k] = v < n;
+                todo[k] = __ballot(valid[k]);
+                e[k] = ring[v % kIndRing];
+            }
+            // rounds up to the first pending entry (one round unless an entry
+            // of the step is placed by an earlier one of the same step)
             for (;;) {
-                const uint64_t act = pend ? todo & ((pend & (0ull - pend)) - 1ull) : todo;
-                if (!act) {
+                uint64_t act[KS];
+                bool seen = false;
+#pragma unroll
+                for (int k = 0; k < KS; ++k) {
+                    const uint64_t pend = __ballot(valid[k] && e[k].x == kIndPend) & todo[k];
+                    act[k] = seen ? 0ull : (pend ? todo[k] & ((pend & (0ull - pend)) - 1ull) : todo[k]);
+                    seen = seen || pend;
+                }
+                uint64_t any = 0;
+#pragma unroll
+                for (int k = 0; k < KS; ++k) any |= act[k];
+                if (!any) {
                     bad = true;
                     break;
                 }
-                const bool me = (act >> lane) & 1u;
-                const uint32_t lo = e.x, hi = e.y;
-                const uint32_t b = (lo >> 24) ^ mir, u = (hi >> 24) ^ mir;
-                const bool ind = me && (b > u || (b == u && (lo & kIndPlaced)));
-                if (me) SF[qof(v)] = lo & ~(0xFu << 20);
-                uint64_t rem = __ballot(ind);
-                if (rem) {
-                    // rank among the inducing lanes with the same b: a ballot per distinct b
-                    uint32_t rank = 0, cnt = 0;
-                    do {
-                        const uint32_t bl = __builtin_amdgcn_readlane(b, __builtin_ctzll(rem));
-                        const uint64_t m = __ballot(b == bl) & rem;
-                        if ((m >> lane) & 1u) {
-                            rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            cnt = __popcll(m);
+                uint32_t b[KS];
+                bool ind[KS];
+                uint64_t rem[KS];
+                uint64_t left = 0;
+#pragma unroll
+                for (int k = 0; k < KS; ++k) {
+                    const bool me = (act[k] >> lane) & 1u;
+                    const uint32_t lo = e[k].x, hi = e[k].y;
+                    b[k] = (lo >> 24) ^ mir;
+                    const uint32_t u = (hi >> 24) ^ mir;
+                    ind[k] = me && (b[k] > u || (b[k] == u && (lo & kIndPlaced)));
+                    if (me) SF[qof(vs + 64 * k + lane)] = lo & ~(0xFu << 20);
+                    rem[k] = __ballot(ind[k]);
+                    left |= rem[k];
+                }
+                if (left) {
+                    // ranks among the inducing entries with the same b, in
+                    // scan order: a round of ballots per distinct b
+                    uint32_t rank[KS] = {}, cnt = 0;
+                    uint32_t tot_of[KS] = {};
+                    while (left) {
+                        uint32_t bl = 0;
+                        bool got = false;
+#pragma unroll
+                        for (int k = 0; k < KS; ++k)
+                            if (!got && rem[k]) {
+                                bl = (uint32_t)__builtin_amdgcn_readlane((int)b[k], __builtin_ctzll(rem[k]));
+                                got = true;
+                            }
+                        uint64_t m[KS];
+                        uint32_t sb = 0;
+#pragma unroll
+                        for (int k = 0; k < KS; ++k) {
+                            m[k] = __ballot(b[k] == bl) & rem[k];
+                            if ((m[k] >> lane) & 1u) {
+                                rank[k] = sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
+                                tot_of[k] = 0;  // set below
+                            }
+                            sb += (uint32_t)__popcll(m[k]);
+                            rem[k] &= ~m[k];
                         }
-                        rem &= ~m;
-                    } while (rem);
-                    const uint32_t idx = lo & kIndIdx, np = (lo >> 20) & 7u;
-                    const uint32_t p = idx ? idx - 1 : n - 1;
-                    // entry of i - 1: T[p-1] = T[i-2] ... and T[p] = T[i-1]
-                    uint32_t plo = p | ((np - 1) << 20) | kIndPlaced | ((hi & 0xFFu) << 24);
-                    uint32_t phi = ((hi >> 8) & 0xFFFFu) | (lo & 0xFF000000u);
-                    if (ind && np == 0) {  // a chain of placed rotations longer than the carried bytes
-                        const uint32_t x = text_prev4(T, n, p + 1);  // T[p-1] .. T[p-4]
-                        plo = p | (3u << 20) | kIndPlaced | ((x & 0xFFu) << 24);
-                        phi = ((x >> 8) & 0xFFFFFFu) | (lo & 0xFF000000u);
+#pragma unroll
+                        for (int k = 0; k < KS; ++k)
+                            if ((m[k] >> lane) & 1u) tot_of[k] = sb;
+                        left = 0;
+#pragma unroll
+                        for (int k = 0; k < KS; ++k) left |= rem[k];
                     }
-                    uint32_t dest = 0;
-                    if (ind) dest = head[b] + rank;
-                    if (ind && rank == 0) head[b] = dest + cnt;
-                    if (__any(ind && dest >= n)) {
+                    (void)cnt;
+                    uint32_t dest[KS];
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) dest[k] = ind[k] ? head[b[k]] + rank[k] : 0u;  // all reads first
+#pragma unroll
+                    for (int k = 0; k < KS; ++k)
+                        if (ind[k] && rank[k] == 0) head[b[k]] = dest[k] + tot_of[k];
+                    bool over = false;
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) over = over || (ind[k] && dest[k] >= n);
+                    if (__any(over)) {
                         bad = true;
                         break;
                     }
-                    if (ind) {
-                        if (dest < v0 + kIndRing) {
-                            ring[dest % kIndRing] = make_uint2(plo, phi);
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) {
+                        if (!ind[k]) continue;
+                        const uint32_t lo = e[k].x, hi = e[k].y;
+                        const uint32_t idx = lo & kIndIdx, np = (lo >> 20) & 7u;
+                        const uint32_t p = idx ? idx - 1 : n - 1;
+                        // entry of i - 1: T[p-1] = T[i-2] ... and T[p] = T[i-1]
+                        uint32_t plo = p | ((np - 1) << 20) | kIndPlaced | ((hi & 0xFFu) << 24);
+                        uint32_t phi = ((hi >> 8) & 0xFFFFu) | (lo & 0xFF000000u);
+                        if (np == 0) {  // a chain of placed rotations longer than the carried bytes
+                            const uint32_t x = text_prev4(T, n, p + 1);  // T[p-1] .. T[p-4]
+                            plo = p | (3u << 20) | kIndPlaced | ((x & 0xFFu) << 24);
+                            phi = ((x >> 8) & 0xFFFFFFu) | (lo & 0xFF000000u);
+                        }
+                        if (dest[k] < v0 + kIndRing) {
+                            ring[dest[k] % kIndRing] = make_uint2(plo, phi);
                         } else {
-                            SF[qof(dest)] = plo;
-                            SH[qof(dest)] = phi;
+                            SF[qof(dest[k])] = plo;
+                            SH[qof(dest[k])] = phi;
                         }
                     }
                 }
-                todo &= ~act;
-                if (!todo) break;
-                e = ring[r];
-                pend = __ballot(valid && e.x == kIndPend) & todo;
+                uint64_t rest = 0;
+#pragma unroll
+                for (int k = 0; k < KS; ++k) {
+                    todo[k] &= ~act[k];
+                    rest |= todo[k];
+                }
+                if (!rest) break;
+#pragma unroll
+                for (int k = 0; k < KS; ++k) e[k] = ring[(vs + 64 * k + lane) % kIndRing];
             }
-            if (bad) break;
         }
+        IND_T(pt_steps);
         if (more && !bad) stage(v0 + kIndBlock);
+        IND_T(pt_stage);
     }
+#if LFM_IND_PROF
+    if (lane == 0 && s < 4)
+        printf("induce prof s %u n %u: total %llu issue %llu steps %llu stage %llu\n", s, n, clock64() - pt_total,
+               pt_issue, pt_steps, pt_stage);
+#endif
+#undef IND_T
     if (bad && lane == 0) B.flags[s] |= kFlagHost;  // the host library redoes the stream
 }
 
@@ -3273,7 +3368,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (!B.it_full) {
         // the other type placed by one scan; the final order in the vals_b area
         B.sfin = B.vals_b;
-        hipLaunchKernelGGL(bwt_place_sorted, dim3(count), dim3(256), 0, st, B);
+        const uint32_t chunks = (B.cap + kPlaceChunk - 1) / kPlaceChunk;
+        hipLaunchKernelGGL(bwt_place_sorted, dim3(8 * chunks * ((count + 7) / 8)), dim3(256), 0, st, B, chunks);
         hipLaunchKernelGGL(bwt_induce, dim3(count), dim3(64), 0, st, B);
         if (!ok()) return LFM_HIP_ERUNTIME;
         B.sa = B.sfin;

@@ -479,7 +479,7 @@ def decode(buf, shape_tczyx=None, dtype=np.uint16, num_threads=-1):
     if shape_tczyx is None:
         import struct
         xyzct = struct.unpack_from("<5I", buf, 2)
-        dtype = NP_OF[buf[42]]
+        dtype = NP_OF[int(np.frombuffer(buf, dtype=np.uint8, count=43)[42])]
         shape_tczyx = (xyzct[4], xyzct[3], xyzct[2], xyzct[1], xyzct[0])
     out = np.empty(shape_tczyx, dtype=dtype)
     _check(lib().lfm_decode_memory(buf, len(buf), out.ctypes.data, num_threads), "lfm_decode_memory")
@@ -495,9 +495,10 @@ def decode_roi(buf, lb, ub, dtype=None, num_threads=-1, out=None):
     returned reshaped.  The library checks the byte count as well."""
     if len(buf) < 43:
         raise ValueError("decode_roi: %d bytes hold no .lfm header" % len(buf))
-    if buf[42] not in NP_OF:
-        raise ValueError("decode_roi: unknown data type %d in the header" % buf[42])
-    fdt = np.dtype(NP_OF[buf[42]])
+    dt = int(np.frombuffer(buf, dtype=np.uint8, count=43)[42])  # (buf may be bytes, a numpy array or a memoryview)
+    if dt not in NP_OF:
+        raise ValueError("decode_roi: unknown data type %d in the header" % dt)
+    fdt = np.dtype(NP_OF[dt])
     if dtype is not None and np.dtype(dtype) != fdt:
         raise ValueError("decode_roi: the file holds %s, not %s" % (fdt, np.dtype(dtype)))
     shape = tuple(int(u) - int(l) + 1 for l, u in zip(lb, ub))[::-1]
