@@ -53,6 +53,9 @@
 #include <vector>
 #include "lfm_hip.h"
 
+#ifndef LFM_HEAP_PROF
+#define LFM_HEAP_PROF 0  // huff_lengths_heap phase clocks by printf (timing variants only)
+#endif
 #ifndef LFM_IND_PROF
 #define LFM_IND_PROF 0  // bwt_induce phase clocks by printf (timing variants only; 0 in the library)
 #endif
@@ -131,7 +134,7 @@ struct Batch {
     uint32_t* bwt_mode;      // per stream: kModeSortA / kModeSortB / kModeFull
     uint32_t* abcnt;         // per stream: A rotations per first byte [256], then B rotations [256]
     uint32_t* sfin;          // the final order of every rotation (bwt_place_sorted / bwt_induce)
-    uint32_t* sfhi;          // bwt_induce's second entry word per position
+    uint2* ent;              // bwt_induce's entries per final position (the keys_a area, free after the sorts)
     uint32_t it_full;        // sort every rotation (no induction): the fallback for ties that need doubling
 };
 
@@ -246,7 +249,6 @@ constexpr int kCrcUnshift = 14;                         // inverse shift by 2^k 
 static_assert(kRleTile == (kRleChunk << (kCrcLevels - 1)) && kRleTile == (1u << kCrcUnshift), "CRC tables");
 
 __constant__ uint32_t c_crc4[4][256];  // 4 zero feeds of a register holding byte v at byte k
-__constant__ uint32_t c_crc_shift[kCrcLevels][32];
 __constant__ uint32_t c_crc_unshift[kCrcUnshift][32];
 
 // 32x32 GF(2) matrix as 32 columns (column k = image of bit k); m is a
@@ -259,14 +261,51 @@ __device__ __forceinline__ uint32_t gf2_apply(const uint32_t* m, uint32_t v)
     return r;
 }
 
+// CRC shift by 32 << l zero bytes as byte tables: Z(v) = T[l][0][v & 255] ^
+// T[l][1][(v >> 8) & 255] ^ T[l][2][(v >> 16) & 255] ^ T[l][3][v >> 24]
+// (four LDS reads instead of a 32-column GF(2) product per lane)
+__constant__ uint32_t c_crc_shb[kCrcLevels][4][256];
+
+__device__ __forceinline__ uint32_t crc_shift_b(const uint32_t (*t)[256], uint32_t v)
+{
+    return t[0][v & 255u] ^ t[1][(v >> 8) & 255u] ^ t[2][(v >> 16) & 255u] ^ t[3][v >> 24];
+}
+
+// The bytes of a chunk as a bitmask: bit i set when byte i equals byte i - 1
+// (bit 0 clear), i < nv, four bytes per word by a zero-byte test of
+// w ^ (w << 8 | previous byte)
+__device__ __forceinline__ uint32_t chunk_eq_mask(const uint32_t (&w)[kRleChunk / 4], uint32_t nv)
+{
+    uint32_t E = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kRleChunk / 4; ++q) {
+        const uint32_t x = w[q], pb = q ? w[q - 1] >> 24 : x & 255u;
+        const uint32_t y = x ^ ((x << 8) | pb);
+        const uint32_t eq = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y)) & 0x80808080u;  // bit 7: byte equal
+        const uint32_t e4 = ((eq >> 7) & 1u) | ((eq >> 14) & 2u) | ((eq >> 21) & 4u) | ((eq >> 28) & 8u);
+        E |= e4 << (4 * q);
+    }
+    return E & ~1u & (nv >= 32 ? ~0u : (1u << nv) - 1u);
+}
+
+__device__ __forceinline__ uint32_t chunk_byte(const uint32_t (&w)[kRleChunk / 4], uint32_t i)
+{
+    uint32_t x = w[0];
+#pragma unroll
+    for (uint32_t q = 1; q < kRleChunk / 4; ++q) x = (i >> 2) == q ? w[q] : x;
+    return (x >> (8 * (i & 3u))) & 255u;
+}
+
 template <bool FROM_IMG>
 __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))) void rle1_crc(Batch B)
 {
     constexpr uint32_t NW = kRleThreads / 64;
     __shared__ uint32_t crc4[4][256];
+    __shared__ uint32_t crcsh[kCrcLevels][4][256];
     // the tile's RLE1 bytes at tout[po ..), po = the stream offset mod 16:
     // tout[0 .. po) holds the previous tile's last partial 16-byte unit
     __shared__ __attribute__((aligned(16))) uint8_t tout[16 + kRleTile + kRleTile / 4 + 64];
+    __shared__ uint8_t junk[kRleThreads];  // where a thread's skipped byte writes land
     __shared__ RunSum wrs[NW];
     __shared__ uint32_t wcnt[NW], wcrc[NW];
     __shared__ RunSum s_carry;
@@ -310,6 +349,8 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
     };
     for (uint32_t i = t; i < 1024; i += kRleThreads) crc4[i >> 8][i & 255] = c_crc4[i >> 8][i & 255];
+    for (uint32_t i = t; i < kCrcLevels * 1024; i += kRleThreads)
+        crcsh[i >> 10][(i >> 8) & 3][i & 255] = c_crc_shb[i >> 10][(i >> 8) & 3][i & 255];
     if (t == 0) {
         s_carry = RunSum{0, 0, 0, 0, 0};
         s_wr = 0;
@@ -358,26 +399,14 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t x = cc ^ __builtin_bswap32(w[q]);
             cc = crc4[3][x >> 24] ^ crc4[2][(x >> 16) & 255u] ^ crc4[1][(x >> 8) & 255u] ^ crc4[0][x & 255u];
         }
-        // chunk run summary
-        RunSum rs{nv, w[0] & 255u, 0, 0, 0};
-        {
-            uint32_t prev = 256, lead = 0, trail = 0;
-            bool lead_open = true;
-#pragma unroll
-            for (uint32_t i = 0; i < kRleChunk; ++i) {
-                if (i < nv) {
-                    const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 255u;
-                    if (lead_open) {
-                        if (c == rs.first) ++lead;
-                        else lead_open = false;
-                    }
-                    trail = c == prev ? trail + 1 : 1;
-                    prev = c;
-                }
-            }
-            rs.last = prev;
-            rs.lead = lead;
-            rs.trail = trail;
+        // chunk run summary from the equal-neighbour mask
+        const uint32_t Ein = chunk_eq_mask(w, nv);
+        const uint32_t b0 = w[0] & 255u;
+        const uint32_t blast = nv == kRleChunk ? w[7] >> 24 : chunk_byte(w, nv ? nv - 1 : 0u);
+        RunSum rs{nv, b0, blast, 0, 0};
+        if (nv) {
+            rs.lead = 1u + (uint32_t)__builtin_ctz(~(Ein >> 1));
+            rs.trail = 1u + (uint32_t)__clz(~(Ein << (32u - nv)));
         }
         // scan of the run summaries: wave, then waves, on top of the carry
         RunSum inc = rs;
@@ -397,28 +426,44 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (w2 < wave) pre = run_combine(pre, o);
         }
         pre = run_combine(pre, exc);
+        // the bzip2 run state at the chunk start: byte ch0 (256: none) in a
+        // run piece of rl0 bytes (a piece restarts every 255 bytes)
         const uint32_t ch0 = pre.len ? pre.last : 256u, rl0 = pre.len ? (pre.trail - 1) % 255 + 1 : 0u;
         const bool has_end = nv && g + nv == L;
-        // the bzip2 run state machine over the chunk; emit(c, l) for every run that ends here
+        const uint32_t valid = nv >= 32 ? ~0u : (1u << nv) - 1u;
+        const uint32_t E = Ein | (nv && b0 == ch0 ? 1u : 0u);
+        // a piece reaching 255 bytes splits only when the carried piece is that long
+        const bool slow = rl0 >= 224 && (E & 1u);
+        // byte i is copied when it is among the first four of its piece, and a
+        // piece of >= 4 bytes ends with its count byte (written before the
+        // next piece's first byte, or at the stream end): with Y = E << 3 | the
+        // carried piece's bytes, r_i >= k <=> bits i .. i + k - 2 of Y set
+        const uint64_t Y = ((uint64_t)E << 3) | (rl0 >= 4 ? 1u : 0u) | (rl0 >= 3 ? 2u : 0u) | (rl0 >= 2 ? 4u : 0u);
+        const uint64_t Q = Y & (Y >> 1) & (Y >> 2);  // bit i: the piece through byte i - 1 has >= 4 bytes
+        const uint32_t S = ~E & valid;               // bytes starting a piece
+        const uint32_t omask = ~(uint32_t)(Q & (Y >> 3)) & valid;
+        const uint32_t cmask = S & (uint32_t)Q;
+        const bool endc = has_end && ((Q >> nv) & 1u);
+        // the same bytes by the sequential state machine (a piece reaches
+        // 255 bytes inside the chunk): emit(byte, is a count byte) in order
         auto walk = [&](auto&& emit) {
-            uint32_t ch = ch0, rl = rl0;
-#pragma unroll
-            for (uint32_t i = 0; i < kRleChunk; ++i) {
-                if (i < nv) {
-                    const uint32_t c = (w[i >> 2] >> (8 * (i & 3))) & 255u;
-                    if (c != ch || rl == 255) {
-                        if (ch < 256) emit(ch, rl);
-                        ch = c;
-                        rl = 1;
-                    } else {
-                        ++rl;
-                    }
-                }
+            uint32_t ch = ch0, r = rl0;
+            for (uint32_t i = 0; i < nv; ++i) {
+                const uint32_t c = chunk_byte(w, i);
+                const bool same = c == ch && r < 255;
+                if (!same && r >= 4) emit(r - 4, true);
+                r = same ? r + 1 : 1u;
+                ch = c;
+                if (r <= 4) emit(c, false);
             }
-            if (has_end) emit(ch, rl);  // flush_RL of the final run
+            if (has_end && r >= 4) emit(r - 4, true);  // flush_RL of the final run
         };
         uint32_t cnt = 0;
-        walk([&](uint32_t, uint32_t l) { cnt += l >= 4 ? 5u : l; });
+        if (!slow) {
+            cnt = (uint32_t)__popc(omask) + (uint32_t)__popc(cmask) + (endc ? 1u : 0u);
+        } else {
+            walk([&](uint32_t, bool) { ++cnt; });
+        }
         uint32_t cinc = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -426,12 +471,12 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             if ((int)lane >= d) cinc += o;
         }
         if (lane == 63) wcnt[wave] = cinc;
-        // tile CRC: tree over the wave's chunks, then over the waves
+        // tile CRC: tree over the wave's chunks (byte tables of the shifts)
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const uint32_t o = __shfl_xor(cc, 1 << k);
             const bool right = (lane >> k) & 1u;
-            cc = gf2_apply(c_crc_shift[k], right ? o : cc) ^ (right ? cc : o);
+            cc = crc_shift_b(crcsh[k], right ? o : cc) ^ (right ? cc : o);
         }
         if (lane == 0) wcrc[wave] = cc;
         __syncthreads();
@@ -441,28 +486,56 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (w2 < wave) base += wcnt[w2];
             total += wcnt[w2];
         }
-        walk([&](uint32_t c, uint32_t l) {
-            const uint8_t b = (uint8_t)c;
-            if (l >= 4) {
-                tout[base] = b; tout[base + 1] = b; tout[base + 2] = b; tout[base + 3] = b;
-                tout[base + 4] = (uint8_t)(l - 4);
-                base += 5;
-            } else {
-                for (uint32_t k = 0; k < l; ++k) tout[base + k] = b;
-                base += l;
+        if (!slow) {
+            // copies in order, the count bytes after (each a few per chunk at most)
+            uint32_t pos = base;
+#pragma unroll
+            for (uint32_t i = 0; i < kRleChunk; ++i) {
+                pos += (cmask >> i) & 1u;
+                const bool of = (omask >> i) & 1u;
+                uint8_t* dst = of ? &tout[pos] : &junk[t];
+                *dst = (uint8_t)(w[i >> 2] >> (8 * (i & 3u)));
+                pos += of ? 1u : 0u;
             }
-        });
+            uint32_t cm = cmask;
+            while (cm) {
+                const uint32_t i = (uint32_t)__builtin_ctz(cm);
+                cm &= cm - 1u;
+                const uint32_t lt = (1u << i) - 1u, m = S & lt;
+                const uint32_t len = m ? i - (31u - (uint32_t)__clz(m)) : rl0 + i;
+                tout[base + (uint32_t)__popc(omask & lt) + (uint32_t)__popc(cmask & lt)] = (uint8_t)(len - 4u);
+            }
+            if (endc) {
+                const uint32_t m = S & valid;
+                const uint32_t len = m ? nv - (31u - (uint32_t)__clz(m)) : rl0 + nv;
+                tout[base + cnt - 1u] = (uint8_t)(len - 4u);
+            }
+        } else {
+            walk([&](uint32_t v, bool) { tout[base++] = (uint8_t)v; });
+        }
         RunSum ncarry{0, 0, 0, 0, 0};
-        uint32_t ncrc = 0;
         if (t == 0) {
             ncarry = s_carry;
-            uint32_t tc = 0;
 #pragma unroll
-            for (uint32_t w2 = 0; w2 < NW; ++w2) {
-                ncarry = run_combine(ncarry, wrs[w2]);
-                tc = gf2_apply(c_crc_shift[6], tc) ^ wcrc[w2];
+            for (uint32_t w2 = 0; w2 < NW; ++w2) ncarry = run_combine(ncarry, wrs[w2]);
+        }
+        // the tile's CRC: wave CRCs shifted by the waves after them (lane
+        // w < 8 of wave 0: (7 - w) * 2048 bytes, levels 6..8), xor-reduced,
+        // on top of the stream CRC shifted by the tile (level 9)
+        uint32_t ncrc = 0;
+        if (wave == 0) {
+            static_assert(NW == 8 && kRleChunk * 64 == (32u << 6), "wave CRC levels");
+            uint32_t x = lane < NW ? wcrc[lane] : 0u;
+            const uint32_t sh = NW - 1 - min(lane, NW - 1);
+#pragma unroll
+            for (int l = 0; l < 3; ++l) {
+                const uint32_t y = crc_shift_b(crcsh[6 + l], x);
+                x = (sh >> l) & 1u ? y : x;
             }
-            ncrc = gf2_apply(c_crc_shift[9], s_crc) ^ tc;
+            x ^= __shfl_xor(x, 1);
+            x ^= __shfl_xor(x, 2);
+            x ^= __shfl_xor(x, 4);
+            ncrc = crc_shift_b(crcsh[9], s_crc) ^ x;
         }
         __syncthreads();
         // whole 16-byte units out (16-byte stores; a unit starting before
@@ -1377,8 +1450,8 @@ __global__ __launch_bounds__(256) void bwt_flag_periodic(Batch B, const uint32_t
 // valid (3 for a sorted rotation, one fewer per induction: a longer chain of
 // placed rotations reads the text), and T[i] is the rotation's bucket.
 // bwt_place_sorted writes the sorted entries to their final positions in
-// sfin / sfhi and kIndPend to every position still to place; bwt_induce then
-// reads nothing else, and overwrites every position with its sort value.
+// `ent` and kIndPend to every position still to place; bwt_induce then
+// reads nothing else, and writes every position's sort value to sfin.
 constexpr uint32_t kIndPend = 0xFFFFFFFFu;  // never an entry: nprev <= 3
 constexpr uint32_t kIndIdx = 0xFFFFFu;      // n < nblock_max < 2^20
 constexpr uint32_t kIndPlaced = 1u << 23;
@@ -1434,7 +1507,7 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks
     const size_t o = (size_t)s * B.cap;
     const uint8_t* T = B.T + o;
     uint32_t* SF = B.sfin + o;
-    uint32_t* SH = B.sfhi + o;
+    uint2* E = B.ent + o;
     // the sorted slots [base, base + kPlaceChunk): sa, then T[i-4 .. i], all
     // loads issued before any is used
     constexpr int K = kPlaceChunk / 256;
@@ -1466,8 +1539,11 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks
             c = T[i];
         }
         const uint32_t qq = (mode == kModeSortA ? q0[c] : p1[c]) + (j - s0[c]);
-        SF[qq] = mode == kModeFull ? v[q] : (v[q] | (3u << 20));
-        SH[qq] = ((x >> 16) & 0xFFu) | (((x >> 8) & 0xFFu) << 8) | ((x & 0xFFu) << 16) | (c << 24);
+        if (mode == kModeFull)
+            SF[qq] = v[q];  // the final order already
+        else
+            E[qq] = make_uint2(v[q] | (3u << 20),
+                               ((x >> 16) & 0xFFu) | (((x >> 8) & 0xFFu) << 8) | ((x & 0xFFu) << 16) | (c << 24));
     }
     // the positions [base, base + kPlaceChunk) still to place: the buckets
     // overlapping the range, from the last one starting at or before base
@@ -1479,29 +1555,44 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks
         else hi = mid - 1;
     }
     for (uint32_t c = lo; c < 256 && q0[c] < end; ++c)
-        for (uint32_t q = max(p0[c], base) + t; q < min(p1[c], end); q += 256) SF[q] = kIndPend;
+        for (uint32_t q = max(p0[c], base) + t; q < min(p1[c], end); q += 256) E[q] = make_uint2(kIndPend, 0u);
 }
 
 // bwt_induce: one wave per stream scans in scan order, in blocks of
 // kIndSlices slices of 64 positions through an LDS ring of two blocks:
 // entries placed into the current or the next block go to the ring, those
-// further ahead to sfin / sfhi; while a block is scanned the next block's
-// entries are loaded (coalesced) and written into the ring after the scan
-// (kIndPend = not placed yet).  The inducing lanes of a slice are ranked per
-// b' with one ballot per distinct b' (the predecessors of a run of sorted
-// rotations take few distinct bytes), so the slots follow the scan order; an
-// entry still pending when its slice is scanned is placed by an earlier lane
-// of the same slice: the slice then runs in rounds up to its first pending lane.
+// further ahead to `ent`; while a block is scanned the next block's entries
+// are loaded (LDS-DMA, 16 bytes per lane) and written into the ring after the
+// scan (kIndPend = not placed yet).  The final values of a block collect in
+// LDS and leave in 16-byte stores: the wave's memory instructions, not its
+// arithmetic, bound the scan (each store stays outstanding for thousands of
+// cycles with every CU storing), so there are few and wide ones.  The
+// inducing lanes of a slice are ranked per b' with one ballot per distinct b'
+// (the predecessors of a run of sorted rotations take few distinct bytes), so
+// the slots follow the scan order; an entry still pending when its slice is
+// scanned is placed by an earlier lane of the same slice: the step then runs
+// in rounds up to its first pending lane.
 constexpr uint32_t kIndSlices = 8;
 constexpr uint32_t kIndBlock = 64 * kIndSlices;
-constexpr int kIndStepSlices = 4;  // slices scanned together (one round of ballots and LDS latencies)
+#ifndef LFM_IND_KS
+#define LFM_IND_KS 4
+#endif
+constexpr int kIndStepSlices = LFM_IND_KS;  // slices scanned together (one round of ballots and LDS latencies)
 constexpr uint32_t kIndRing = 2 * kIndBlock;
 
-// LDS-DMA of one dword per lane into LDS at `lds` + 4 * lane, from L2 (sc1:
-// the entries were written by this wave earlier).  Inline asm: the compiler
-// does not track the DMA, so nothing of it ties up VGPRs while the wave works
+// LDS-DMA of 16 bytes per lane into LDS at `lds` + 16 * lane, from L2 (sc1:
+// the entries were written by this wave earlier, and a line may sit in the
+// L1 from the previous block's load).  Inline asm: the compiler does not
+// track the DMA, so nothing of it ties up VGPRs while the wave works
 // (bwt_induce waits with vm_drain before it reads the staged entries).
-__device__ __forceinline__ void glds4(const uint32_t* g, const void* lds)
+__device__ __forceinline__ void glds16(const void* g, const void* lds)
+{
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1" ::"s"(m0), "v"(g) : "memory", "m0");
+}
+
+__device__ __forceinline__ void glds4(const uint32_t* g, const void* lds)  // 4 bytes per lane
 {
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)lds);
@@ -1512,9 +1603,10 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 
 __global__ __launch_bounds__(64) void bwt_induce(Batch B)
 {
-    __shared__ uint32_t head[256];  // next free scan position of bucket u's placed part
+    __shared__ uint32_t head[256];            // next free scan position of bucket u's placed part
     __shared__ uint2 ring[kIndRing];
-    __shared__ uint32_t stg[2][kIndBlock];  // the next block's entries as loaded (lo, hi)
+    __shared__ __attribute__((aligned(16))) uint2 stg[kIndBlock + 32];      // the next block's entries, in q order
+    __shared__ __attribute__((aligned(16))) uint32_t fin[kIndBlock + 256];  // the block's final values, in q order
     const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
@@ -1524,7 +1616,7 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
     const uint32_t mir = rev ? 255u : 0u;
     const size_t o = (size_t)s * B.cap;
     uint32_t* SF = B.sfin + o;
-    uint32_t* SH = B.sfhi + o;
+    uint2* E = B.ent + o;
     const uint8_t* T = B.T + o;
     {  // head[u] = scan-order start of bucket u (its placed part comes first)
         uint32_t nt[4], l = 0;
@@ -1547,31 +1639,63 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
         }
     }
     for (uint32_t i = lane; i < kIndRing; i += 64) ring[i].x = kIndPend;
-    // position in sfin of scan position v
+    // position in `ent` / sfin of scan position v.  A block [vb, vb + kIndBlock)
+    // covers q in [qwin(vb), qwin(vb) + kIndBlock); stg holds it from q =
+    // qwin & ~1, fin from q = qwin & ~3 (16-byte aligned transfers)
     const uint32_t qa = rev ? n - 1 : 0u;
     auto qof = [&](uint32_t v) { return rev ? qa - v : v; };
-    auto issue = [&](uint32_t vb) {  // the block at vb into stg by LDS-DMA (clamped: every lane loads)
+    auto qwin = [&](uint32_t vb) { return rev ? (int)n - (int)kIndBlock - (int)vb : (int)vb; };
+    // slot of the block's t-th position in a buffer starting d before qwin
+    auto wof = [&](uint32_t t, int d) { return rev ? (uint32_t)d + kIndBlock - 1 - t : t; };
+    const int qmax = (int)B.cap - 2;
+    auto issue = [&](uint32_t vb) {  // the block at vb into stg (clamped: every lane loads)
+        const int qw = qwin(vb), qs = qw & ~1;
 #pragma unroll
-        for (uint32_t k = 0; k < kIndSlices; ++k) {
-            const uint32_t q = qof(min(vb + 64 * k + lane, n - 1));
-            glds4(SF + q, &stg[0][64 * k]);
-            glds4(SH + q, &stg[1][64 * k]);
+        for (uint32_t j = 0; j < kIndBlock / 128; ++j) {
+            const int q = min(max(qs + (int)(128 * j + 2 * lane), 0), qmax);
+            glds16(E + q, &stg[128 * j]);
+        }
+        if (qw & 1) {  // the block's last slot: entry qs + kIndBlock, one dword per lane 0 and 1
+            const int q = min(max(qs + (int)kIndBlock, 0), qmax);
+            glds4((const uint32_t*)(E + q) + min(lane, 1u), &stg[kIndBlock]);
         }
     };
     auto stage = [&](uint32_t vb) {  // into the ring: entries known when loaded
+        const int d = qwin(vb) & 1;
         vm_drain();
+        uint2 x[kIndSlices];
+#pragma unroll
+        for (uint32_t k = 0; k < kIndSlices; ++k) x[k] = stg[wof(64 * k + lane, d)];
+        asm volatile("" ::: "memory");  // every read issued before the first write
 #pragma unroll
         for (uint32_t k = 0; k < kIndSlices; ++k) {
             const uint32_t v = vb + 64 * k + lane;
-            const uint32_t lo = stg[0][64 * k + lane], hi = stg[1][64 * k + lane];
-            if (v < n && lo != kIndPend) ring[v % kIndRing] = make_uint2(lo, hi);
+            if (v < n && x[k].x != kIndPend) ring[v % kIndRing] = x[k];
+        }
+    };
+    auto flush = [&](uint32_t vb) {  // the block's final values to sfin, 16 bytes per lane
+        const int qw = qwin(vb), qf = qw & ~3;
+        const int lo = max(qw, 0), hi = min(qw + (int)kIndBlock, (int)n);  // the block's positions
+        for (uint32_t j = 0; j < (kIndBlock + 256) / 256 && (int)(256 * j) < hi - qf; ++j) {
+            const uint32_t w = 256 * j + 4 * lane;
+            const uint4 f = *(const uint4*)&fin[w];
+            const int q = qf + (int)w;
+            if (q >= lo && q + 3 < hi) {
+                *(uint4*)(SF + q) = f;
+            } else {
+                const uint32_t fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (q + r >= lo && q + r < hi) SF[q + r] = fv[r];
+            }
         }
     };
     __syncthreads();
     issue(0);
     stage(0);
 #if LFM_IND_PROF
-    unsigned long long pt0 = 0, pt_issue = 0, pt_steps = 0, pt_stage = 0, pt_total = clock64();
+    unsigned long long pt0 = 0, pt_issue = 0, pt_steps = 0, pt_stage = 0, pt_flush = 0, pt_total = clock64();
+    uint32_t c_steps = 0, c_rounds = 0, c_dist = 0, c_text = 0, c_far = 0, c_ind = 0;
 #define IND_T(x) do { const unsigned long long t_ = clock64(); x += t_ - pt0; pt0 = t_; } while (0)
 #else
 #define IND_T(x) do { } while (0)
@@ -1592,37 +1716,49 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
         for (uint32_t vs = v0; vs < min(n, v0 + kIndBlock) && !bad; vs += 64 * kIndStepSlices) {
             constexpr int KS = kIndStepSlices;
             uint2 e[KS];
-            bool valid[KS];
             uint64_t todo[KS];
 #pragma unroll
             for (int k = 0; k < KS; ++k) {
                 const uint32_t v = vs + 64 * k + lane;
-                valid[k] = v < n;
-                todo[k] = __ballot(valid[k]);
+                todo[k] = __ballot(v < n);
                 e[k] = ring[v % kIndRing];
             }
-            // rounds up to the first pending entry (one round unless an entry
-            // of the step is placed by an earlier one of the same step)
+#if LFM_IND_PROF
+            ++c_steps;
+#endif
+            // rounds up to the first pending entry: one round unless an entry
+            // of the step is placed by an earlier one of the same step
             for (;;) {
-                uint64_t act[KS];
-                bool seen = false;
+#if LFM_IND_PROF
+                ++c_rounds;
+#endif
+                uint64_t act[KS], pend[KS], anyp = 0;
 #pragma unroll
                 for (int k = 0; k < KS; ++k) {
-                    const uint64_t pend = __ballot(valid[k] && e[k].x == kIndPend) & todo[k];
-                    act[k] = seen ? 0ull : (pend ? todo[k] & ((pend & (0ull - pend)) - 1ull) : todo[k]);
-                    seen = seen || pend;
+                    pend[k] = __ballot(e[k].x == kIndPend) & todo[k];
+                    anyp |= pend[k];
                 }
-                uint64_t any = 0;
+                if (!anyp) {
 #pragma unroll
-                for (int k = 0; k < KS; ++k) any |= act[k];
-                if (!any) {
-                    bad = true;
-                    break;
+                    for (int k = 0; k < KS; ++k) act[k] = todo[k];
+                } else {
+                    bool seen = false;
+                    uint64_t any = 0;
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) {
+                        const uint64_t pk = pend[k];
+                        act[k] = seen ? 0ull : (pk ? todo[k] & ((pk & (0ull - pk)) - 1ull) : todo[k]);
+                        seen = seen || pk;
+                        any |= act[k];
+                    }
+                    if (!any) {
+                        bad = true;
+                        break;
+                    }
                 }
                 uint32_t b[KS];
                 bool ind[KS];
-                uint64_t rem[KS];
-                uint64_t left = 0;
+                uint64_t rem[KS], left = 0;
 #pragma unroll
                 for (int k = 0; k < KS; ++k) {
                     const bool me = (act[k] >> lane) & 1u;
@@ -1630,16 +1766,24 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                     b[k] = (lo >> 24) ^ mir;
                     const uint32_t u = (hi >> 24) ^ mir;
                     ind[k] = me && (b[k] > u || (b[k] == u && (lo & kIndPlaced)));
-                    if (me) SF[qof(vs + 64 * k + lane)] = lo & ~(0xFu << 20);
+                    if (me) fin[wof(vs - v0 + 64 * k + lane, qwin(v0) & 3)] = lo & ~(0xFu << 20);
                     rem[k] = __ballot(ind[k]);
                     left |= rem[k];
                 }
                 if (left) {
                     // ranks among the inducing entries with the same b, in
                     // scan order: a round of ballots per distinct b
-                    uint32_t rank[KS] = {}, cnt = 0;
-                    uint32_t tot_of[KS] = {};
+                    uint32_t rank[KS], tot_of[KS];
+                    bool inm[KS];
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) {
+                        rank[k] = 0;
+                        tot_of[k] = 0;
+                    }
                     while (left) {
+#if LFM_IND_PROF
+                        ++c_dist;
+#endif
                         uint32_t bl = 0;
                         bool got = false;
 #pragma unroll
@@ -1648,62 +1792,72 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                                 bl = (uint32_t)__builtin_amdgcn_readlane((int)b[k], __builtin_ctzll(rem[k]));
                                 got = true;
                             }
-                        uint64_t m[KS];
                         uint32_t sb = 0;
-#pragma unroll
-                        for (int k = 0; k < KS; ++k) {
-                            m[k] = __ballot(b[k] == bl) & rem[k];
-                            if ((m[k] >> lane) & 1u) {
-                                rank[k] = sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0u));
-                                tot_of[k] = 0;  // set below
-                            }
-                            sb += (uint32_t)__popcll(m[k]);
-                            rem[k] &= ~m[k];
-                        }
-#pragma unroll
-                        for (int k = 0; k < KS; ++k)
-                            if ((m[k] >> lane) & 1u) tot_of[k] = sb;
                         left = 0;
 #pragma unroll
-                        for (int k = 0; k < KS; ++k) left |= rem[k];
+                        for (int k = 0; k < KS; ++k) {
+                            const uint64_t m = __ballot(b[k] == bl) & rem[k];
+                            inm[k] = (m >> lane) & 1u;
+                            const uint32_t r =
+                                sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            rank[k] = inm[k] ? r : rank[k];
+                            sb += (uint32_t)__popcll(m);
+                            rem[k] &= ~m;
+                            left |= rem[k];
+                        }
+#pragma unroll
+                        for (int k = 0; k < KS; ++k) tot_of[k] = inm[k] ? sb : tot_of[k];
                     }
-                    (void)cnt;
                     uint32_t dest[KS];
 #pragma unroll
-                    for (int k = 0; k < KS; ++k) dest[k] = ind[k] ? head[b[k]] + rank[k] : 0u;  // all reads first
+                    for (int k = 0; k < KS; ++k) dest[k] = head[b[k]] + rank[k];  // all reads first
 #pragma unroll
                     for (int k = 0; k < KS; ++k)
                         if (ind[k] && rank[k] == 0) head[b[k]] = dest[k] + tot_of[k];
-                    bool over = false;
+                    bool over = false, np0 = false;
+                    uint32_t plo[KS], phi[KS];
 #pragma unroll
-                    for (int k = 0; k < KS; ++k) over = over || (ind[k] && dest[k] >= n);
+                    for (int k = 0; k < KS; ++k) {
+                        over = over || (ind[k] && dest[k] >= n);
+                        // entry of i - 1: T[p-1] = T[i-2] ... and T[p] = T[i-1]
+                        const uint32_t lo = e[k].x, hi = e[k].y;
+                        const uint32_t idx = lo & kIndIdx, np = (lo >> 20) & 7u;
+                        const uint32_t p = idx ? idx - 1 : n - 1;
+                        plo[k] = p | ((np - 1) << 20) | kIndPlaced | ((hi & 0xFFu) << 24);
+                        phi[k] = ((hi >> 8) & 0xFFFFu) | (lo & 0xFF000000u);
+                        np0 = np0 || (ind[k] && np == 0);
+                    }
                     if (__any(over)) {
                         bad = true;
                         break;
                     }
+                    if (__any(np0)) {
 #pragma unroll
-                    for (int k = 0; k < KS; ++k) {
-                        if (!ind[k]) continue;
-                        const uint32_t lo = e[k].x, hi = e[k].y;
-                        const uint32_t idx = lo & kIndIdx, np = (lo >> 20) & 7u;
-                        const uint32_t p = idx ? idx - 1 : n - 1;
-                        // entry of i - 1: T[p-1] = T[i-2] ... and T[p] = T[i-1]
-                        uint32_t plo = p | ((np - 1) << 20) | kIndPlaced | ((hi & 0xFFu) << 24);
-                        uint32_t phi = ((hi >> 8) & 0xFFFFu) | (lo & 0xFF000000u);
-                        if (np == 0) {  // a chain of placed rotations longer than the carried bytes
+                        for (int k = 0; k < KS; ++k) {
+                            const uint32_t lo = e[k].x;
+                            if (!ind[k] || ((lo >> 20) & 7u)) continue;
+                            // a chain of placed rotations longer than the carried bytes
+                            const uint32_t idx = lo & kIndIdx, p = idx ? idx - 1 : n - 1;
                             const uint32_t x = text_prev4(T, n, p + 1);  // T[p-1] .. T[p-4]
-                            plo = p | (3u << 20) | kIndPlaced | ((x & 0xFFu) << 24);
-                            phi = ((x >> 8) & 0xFFFFFFu) | (lo & 0xFF000000u);
-                        }
-                        if (dest[k] < v0 + kIndRing) {
-                            ring[dest[k] % kIndRing] = make_uint2(plo, phi);
-                        } else {
-                            SF[qof(dest[k])] = plo;
-                            SH[qof(dest[k])] = phi;
+                            plo[k] = p | (3u << 20) | kIndPlaced | ((x & 0xFFu) << 24);
+                            phi[k] = ((x >> 8) & 0xFFFFFFu) | (lo & 0xFF000000u);
+#if LFM_IND_PROF
+                            ++c_text;
+#endif
                         }
                     }
+#pragma unroll
+                    for (int k = 0; k < KS; ++k) {
+                        const bool near = dest[k] < v0 + kIndRing;
+#if LFM_IND_PROF
+                        c_ind += ind[k];
+                        c_far += ind[k] && !near;
+#endif
+                        if (ind[k] && near) ring[dest[k] % kIndRing] = make_uint2(plo[k], phi[k]);
+                        if (ind[k] && !near) E[qof(dest[k])] = make_uint2(plo[k], phi[k]);
+                    }
                 }
+                if (!anyp) break;
                 uint64_t rest = 0;
 #pragma unroll
                 for (int k = 0; k < KS; ++k) {
@@ -1716,13 +1870,16 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
             }
         }
         IND_T(pt_steps);
+        if (!bad) flush(v0);
+        IND_T(pt_flush);
         if (more && !bad) stage(v0 + kIndBlock);
         IND_T(pt_stage);
     }
 #if LFM_IND_PROF
     if (lane == 0 && s < 4)
-        printf("induce prof s %u n %u: total %llu issue %llu steps %llu stage %llu\n", s, n, clock64() - pt_total,
-               pt_issue, pt_steps, pt_stage);
+        printf("induce prof s %u n %u mode %u: total %llu issue %llu steps %llu flush %llu stage %llu | steps %u "
+               "rounds %u distinct %u induced(lane0) %u text %u far %u\n", s, n, mode, clock64() - pt_total,
+               pt_issue, pt_steps, pt_flush, pt_stage, c_steps, c_rounds, c_dist, c_ind, c_text, c_far);
 #endif
 #undef IND_T
     if (bad && lane == 0) B.flags[s] |= kFlagHost;  // the host library redoes the stream
@@ -1948,11 +2105,20 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
         // serial loop over them (~27 per window, a readlane each) was
         // scalar-unit bound
         {
+            // only the words from the lowest to the highest first-occurrence
+            // rank carry bits that count (usually one or two of the eight)
             const bool isF = valid && !has_prev;
             const uint32_t pw = P0 >> 5, pb = P0 & 31u;
-            uint32_t cnt = 0;
+            uint32_t wlo = 8, whi = 0;
 #pragma unroll
             for (uint32_t wd = 0; wd < 8; ++wd) {
+                if (__ballot(isF && pw == wd)) {
+                    wlo = min(wlo, wd);
+                    whi = wd;
+                }
+            }
+            uint32_t cnt = 0;
+            for (uint32_t wd = wlo; wd <= whi; ++wd) {
                 const uint32_t oh = (isF && pw == wd) ? (1u << pb) : 0u;
                 const uint32_t pre = wave_or_scan_excl32(oh);
                 const uint32_t above = wd > pw ? ~0u : (wd == pw ? (pb == 31 ? 0u : ~0u << (pb + 1)) : 0u);
@@ -2408,8 +2574,36 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             }
             return z;
         };
+        // upheap for the initial inserts (each climbs about log2(i) levels):
+        // every ancestor read first (one LDS latency), then the moves decided
+        // from registers; returns the final position
+        auto upheap_init = [&](uint32_t z, Ent k) {
+            constexpr int D = 10;  // z < 1024: nine levels to the root, then the sentinel entry 0
+            Ent anc[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) anc[j] = ent(z >> (j + 1));
+            bool go = true;
+            uint32_t zf = z;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                go = go && k < (anc[j] & kW);  // the sentinel 0 stops it
+                if (go) {
+                    ent(z >> j) = anc[j];
+                    zf = z >> (j + 1);
+                }
+                if (!__any(go)) break;
+            }
+            ent(zf) = k;
+            return zf;
+        };
+#if LFM_HEAP_PROF
+        unsigned long long hp_t0 = clock64(), hp_load = 0, hp_up = 0, hp_merge = 0, hp_t = 0;
+#endif
         int retries = 0, nNodes = A;
         while (true) {
+#if LFM_HEAP_PROF
+            hp_t = clock64();
+#endif
             // leaves at heap positions 1 .. A first (an insertion's upheap only
             // touches positions below it), then inserted in order
             ent(0) = 0;
@@ -2431,7 +2625,13 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
                     if (i + 1 <= A) ent(i + 1) = ((Ent)w1 << 15) | (Ent)(i + 1);
                 }
             }
-            for (int i = 1; i <= A; ++i) upheap((uint32_t)i, ent(i));
+#if LFM_HEAP_PROF
+            { const unsigned long long t_ = clock64(); hp_load += t_ - hp_t; hp_t = t_; }
+#endif
+            for (int i = 1; i <= A; ++i) upheap_init((uint32_t)i, ent(i));
+#if LFM_HEAP_PROF
+            { const unsigned long long t_ = clock64(); hp_up += t_ - hp_t; hp_t = t_; }
+#endif
             int nHeap = A;
             nNodes = A;
             uint32_t tooLong = 0;
@@ -2452,9 +2652,15 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
                 ++nHeap;
                 top = upheap((uint32_t)nHeap, kn) == 1u ? kn : r2;
             }
+#if LFM_HEAP_PROF
+            { const unsigned long long t_ = clock64(); hp_merge += t_ - hp_t; hp_t = t_; }
+#endif
             if (!tooLong) break;
             ++retries;
         }
+#if LFM_HEAP_PROF
+        const unsigned long long hp_t1 = clock64();
+#endif
         if (retries) atomicAdd(B.wide_cnt + 1, (uint32_t)retries);  // statistics (LFM_BZ2_STATS)
         // depths top-down (a parent is created after its children)
         dep(nNodes) = 0;
@@ -2474,6 +2680,11 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             }
         }
         for (int i = 1; i <= A; ++i) len[i - 1] = (uint8_t)dep(i);
+#if LFM_HEAP_PROF
+        if (lane == 0 && s < 3 && tb == 0)
+            printf("heap prof s %u A %d retries %d: total %llu load %llu upinit %llu merge %llu depth %llu\n", s, A,
+                   retries, clock64() - hp_t0, hp_load, hp_up, hp_merge, clock64() - hp_t1);
+#endif
     }
 }
 
@@ -2953,6 +3164,7 @@ uint32_t host_crc_table[256];
 uint32_t host_crc4[4][256];
 uint32_t host_crc_shift[kCrcLevels][32];
 uint32_t host_crc_unshift[kCrcUnshift][32];
+uint32_t host_crc_shb[kCrcLevels][4][256];  // host_crc_shift as byte tables
 bool crc_ready = false;
 
 void ensure_crc_table()
@@ -3002,6 +3214,9 @@ void ensure_crc_table()
     }
     std::memcpy(host_crc_shift[0], z, sizeof(z));
     for (int l = 1; l < kCrcLevels; ++l) mat_square(host_crc_shift[l - 1], host_crc_shift[l]);
+    for (int l = 0; l < kCrcLevels; ++l)
+        for (uint32_t j = 0; j < 4; ++j)
+            for (uint32_t v = 0; v < 256; ++v) host_crc_shb[l][j][v] = mat_apply(host_crc_shift[l], v << (8 * j));
     for (int k = 0; k < 32; ++k) host_crc_unshift[0][k] = unfeed0(1u << k);
     for (int l = 1; l < kCrcUnshift; ++l) mat_square(host_crc_unshift[l - 1], host_crc_unshift[l]);
     crc_ready = true;
@@ -3075,7 +3290,7 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * align_up(raw_cap, 16), 256);   // raw
     b += align_up(N, 256);                                      // T
     b += 2 * align_up(N * 8, 256);                              // keys
-    b += 7 * align_up(N * 4, 256);                              // vals_a, sa, rank, vals_b, cl0, cl1, sfhi
+    b += 6 * align_up(N * 4, 256);                              // vals_a, sa, rank, vals_b, cl0, cl1
     b += align_up(N, 256);                                      // uflag
     b += align_up((size_t)nstreams * (cap + 8) * 2, 256);       // mtfv
     b += 2 * align_up((size_t)nstreams * sel_cap, 256);         // sel, sel_mtf
@@ -3109,7 +3324,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (crc_dev != dev) {
         if (hipMemcpyToSymbol(HIP_SYMBOL(c_crc_table), host_crc_table, sizeof(host_crc_table)) != hipSuccess ||
             hipMemcpyToSymbol(HIP_SYMBOL(c_crc4), host_crc4, sizeof(host_crc4)) != hipSuccess ||
-            hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shift), host_crc_shift, sizeof(host_crc_shift)) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shb), host_crc_shb, sizeof(host_crc_shb)) != hipSuccess ||
             hipMemcpyToSymbol(HIP_SYMBOL(c_crc_unshift), host_crc_unshift, sizeof(host_crc_unshift)) != hipSuccess)
             return LFM_HIP_ERUNTIME;
         crc_dev = dev;
@@ -3154,7 +3369,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.cl0 = (uint32_t*)take(N * 4);
     B.cl1 = (uint32_t*)take(N * 4);
     B.uflag = take(N);
-    B.sfhi = (uint32_t*)take(N * 4);
     B.mtfv = (uint16_t*)take((size_t)count * (B.cap + 8) * 2);
     B.sel = take((size_t)count * B.sel_cap);
     B.sel_mtf = take((size_t)count * B.sel_cap);
@@ -3368,6 +3582,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     if (!B.it_full) {
         // the other type placed by one scan; the final order in the vals_b area
         B.sfin = B.vals_b;
+        B.ent = (uint2*)B.keys_a;
         const uint32_t chunks = (B.cap + kPlaceChunk - 1) / kPlaceChunk;
         hipLaunchKernelGGL(bwt_place_sorted, dim3(8 * chunks * ((count + 7) / 8)), dim3(256), 0, st, B, chunks);
         hipLaunchKernelGGL(bwt_induce, dim3(count), dim3(64), 0, st, B);
