@@ -1029,7 +1029,12 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
     if (c >= nch) return;
     static_assert(IPT == 2 || IPT == 4 || IPT == 8, "flags are packed 2, 4 or 8 per thread");
-    using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
+#ifndef LFM_CS_BITONIC
+#define LFM_CS_BITONIC 0
+#endif
+    using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t,
+                                     LFM_CS_BITONIC ? rocprim::block_sort_algorithm::bitonic_sort
+                                                    : rocprim::block_sort_algorithm::merge_sort>;
     using ExK = rocprim::block_exchange<uint64_t, TH, IPT>;
     using ExV = rocprim::block_exchange<uint32_t, TH, IPT>;
     constexpr uint32_t NI = TH * IPT;
@@ -1083,7 +1088,8 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     __syncthreads();
     ExV().striped_to_blocked(v, v, sm.ev);
     __syncthreads();
-    Sort().sort(k, v, sm.s, m);
+    if constexpr (LFM_CS_BITONIC) Sort().sort(k, v, sm.s);  // the padding keys (~0, never a text prefix) sort last
+    else Sort().sort(k, v, sm.s, m);
     __syncthreads();
     sm.x.first[t] = k[0];
     sm.x.last[t] = k[IPT - 1];
@@ -2109,14 +2115,9 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
             // rank carry bits that count (usually one or two of the eight)
             const bool isF = valid && !has_prev;
             const uint32_t pw = P0 >> 5, pb = P0 & 31u;
-            uint32_t wlo = 8, whi = 0;
-#pragma unroll
-            for (uint32_t wd = 0; wd < 8; ++wd) {
-                if (__ballot(isF && pw == wd)) {
-                    wlo = min(wlo, wd);
-                    whi = wd;
-                }
-            }
+            const uint32_t wbit = isF ? 1u << pw : 0u;
+            const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)(wave_or_scan_excl32(wbit) | wbit), 63);
+            const uint32_t wlo = wm ? (uint32_t)__builtin_ctz(wm) : 8u, whi = wm ? 31u - (uint32_t)__clz(wm) : 0u;
             uint32_t cnt = 0;
             for (uint32_t wd = wlo; wd <= whi; ++wd) {
                 const uint32_t oh = (isF && pw == wd) ? (1u << pb) : 0u;
@@ -2183,17 +2184,39 @@ constexpr int kRle2Threads = 256;
 constexpr uint32_t kRle2Per = 64;                        // m values per thread and tile
 constexpr uint32_t kRle2Tile = kRle2Threads * kRle2Per;  // 16384
 
-// One workgroup per stream walks it in tiles of 16384 MTF values: per tile a
-// scan carries the pending zero run into each thread's 64 values, the
-// RUNA/RUNB / v+1 symbols are written into an LDS copy of the tile's output
-// (outputs <= inputs + the digits of one carried run + EOB) and copied out
-// with coalesced stores; the run pending at the tile end carries over.
-__global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
+// One workgroup per stream walks it in tiles of 16384 MTF values, 64 per
+// thread.  A thread's zero values are a 64-bit mask; the zero run pending at
+// each thread's first value comes from a scan (trailing zeros, all zero) over
+// the tile on top of the run carried from the previous tiles.  Every nonzero
+// value v ends the zero run before it: the run's RUNA / RUNB digits, then
+// v + 1, go into an LDS copy of the tile's output (placed by a scan of the
+// counts; the digits of a run of z zeros are the bits of z + 1 below its top
+// bit, lowest first) and out with coalesced stores.  Frequencies: RUNA / RUNB
+// and the four hottest symbols in registers, the others by LDS atomics.
+__device__ __forceinline__ uint64_t zero_byte_mask64(const uint32_t (&q)[kRle2Per / 4])
+{
+    uint64_t Z = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kRle2Per / 4; ++k) {
+        const uint32_t y = q[k];
+        const uint32_t z = ~((((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y)) & 0x80808080u;  // bit 7: byte zero
+        const uint32_t z4 = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        Z |= (uint64_t)z4 << (4 * k);
+    }
+    return Z;
+}
+
+#ifndef LFM_RLE2_WPE
+#define LFM_RLE2_WPE 4
+#endif
+__global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(LFM_RLE2_WPE))) void rle2(Batch B)
 {
     constexpr uint32_t NW = kRle2Threads / 64;
     __shared__ uint32_t wz[NW], wa[NW], wc[NW];  // per-wave scan totals
     __shared__ uint32_t freq[kMaxAlpha];
+    __shared__ uint32_t junk32[kRle2Threads];
     __shared__ uint16_t tile_out[kRle2Tile + 64];
+    __shared__ uint16_t junk16[kRle2Threads];
     __shared__ uint32_t s_carry, s_wr;
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
@@ -2209,8 +2232,8 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         s_carry = 0;
         s_wr = 0;
     }
-    uint32_t nrunA = 0, nrunB = 0;  // RUNA / RUNB, the hottest symbols, counted here (two scalars:
-                                    // an array indexed by the symbol lived in scratch memory)
+    uint32_t nrunA = 0, nrunB = 0;
+    uint64_t hot = 0;  // symbols 2 .. 5 (values 1 .. 4): 16-bit counters
     // zero-run scan element: (trailing zeros, all zeros); a then b
     auto zcomb = [](uint32_t atz, uint32_t aaz, uint32_t btz, uint32_t baz, uint32_t& rtz, uint32_t& raz) {
         rtz = baz ? atz + btz : btz;
@@ -2235,21 +2258,11 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
             q[4 * i] = nq[i].x; q[4 * i + 1] = nq[i].y; q[4 * i + 2] = nq[i].z; q[4 * i + 3] = nq[i].w;
         }
         load_vals(tb + kRle2Tile);
-        auto each = [&](auto&& f) {
-#pragma unroll
-            for (uint32_t i = 0; i < kRle2Per; ++i)
-                if (i < len) f((q[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-        };
+        const uint64_t valid = len >= 64 ? ~0ull : (1ull << len) - 1ull;
+        const uint64_t Z = zero_byte_mask64(q) & valid, NZ = ~Z & valid;
         // chunk summary: trailing zeros, all-zero (empty chunks pass the carry through)
-        // (the per-value updates are selects: with `++x` in one branch and
-        // `++y` in the other the compiler merged them into one store through
-        // a selected pointer and kept the counters in scratch memory)
-        uint32_t tz = 0, az = 1;
-        each([&](uint32_t v) {
-            const bool zv = v == 0;
-            tz = zv ? tz + 1 : 0u;
-            az = zv ? az : 0u;
-        });
+        const uint32_t az = NZ == 0ull ? 1u : 0u;
+        const uint32_t tz = az ? len : (uint32_t)__clzll(NZ << (64u - len));
         // inclusive scan over the wave, then the waves before
         uint32_t itz = tz, iaz = az;
 #pragma unroll
@@ -2272,17 +2285,18 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         uint32_t tile_end_zeros = tile_carry, tez = 1;
         for (uint32_t w2 = 0; w2 < NW; ++w2) zcomb(tile_end_zeros, tez, wz[w2], wa[w2], tile_end_zeros, tez);
         const bool has_last = last_tile && len && c1 == n;
-        uint32_t z = carry, w = 0;
-        each([&](uint32_t v) {
-            const bool zv = v == 0;
-            const uint32_t d = z ? run_digits(z) : 0u;
-            w = zv ? w : w + d + 1u;
-            z = zv ? z + 1u : 0u;
-        });
-        if (has_last) {
-            if (z) w += run_digits(z);
-            ++w;  // EOB
-        }
+        // zero runs ending here: at a nonzero value after a zero (or after
+        // the carried zeros), and the stream's final run
+        const uint64_t R = NZ & ((Z << 1) | (carry ? 1ull : 0ull));
+        const uint32_t zend = az ? carry + len : tz;  // zeros at the chunk end (the stream's final run when has_last)
+        auto run_len = [&](uint32_t i) {  // zeros before the nonzero value i
+            const uint64_t below = NZ & ((1ull << i) - 1ull);
+            return below ? i - 1u - (63u - (uint32_t)__clzll(below)) : carry + i;
+        };
+        uint32_t ndig = 0;
+        for (uint64_t r = R; r; r &= r - 1ull) ndig += run_digits(run_len((uint32_t)__builtin_ctzll(r)));
+        const uint32_t dend = has_last && zend ? run_digits(zend) : 0u;
+        const uint32_t w = (uint32_t)__popcll(NZ) + ndig + dend + (has_last ? 1u : 0u);
         // output offsets: scan of the counts
         uint32_t ic = w;
 #pragma unroll
@@ -2297,34 +2311,45 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
             if (w2 < wave) wr += wc[w2];
             tile_total += wc[w2];
         }
-        auto emit = [&](uint32_t v) {
-            tile_out[wr++] = (uint16_t)v;
-            if (v < 2) {
-                nrunA += v == 0;
-                nrunB += v == 1;
-            } else {
-                atomicAdd(&freq[v], 1u);
-            }
+        // the digits of a run of z zeros at p .. p + d - 1
+        auto digits = [&](uint32_t p, uint32_t z) {
+            const uint32_t d = run_digits(z), x = z + 1u;
+            const uint32_t nb = (uint32_t)__popc(x & ((1u << d) - 1u));
+            nrunB += nb;
+            nrunA += d - nb;
+            for (uint32_t k = 0; k < d; ++k) tile_out[p + k] = (uint16_t)((x >> k) & 1u);
         };
-        auto zeros = [&](uint32_t zz) {
-            uint32_t zp = zz - 1;
-            while (true) {
-                emit((zp & 1) ? kRunB : kRunA);
-                if (zp < 2) break;
-                zp = (zp - 2) / 2;
+        // symbols v + 1: one write per value (zeros into a junk slot), the
+        // position advanced past the digits of the run each one ends
+        {
+            uint32_t pos = wr, z = carry;
+#pragma unroll
+            for (uint32_t i = 0; i < kRle2Per; ++i) {
+                const uint32_t v = (q[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                const bool nz = (NZ >> i) & 1u;
+                pos += nz && z ? run_digits(z) : 0u;
+                uint16_t* dst = nz ? &tile_out[pos] : &junk16[t];
+                *dst = (uint16_t)(v + 1u);
+                uint32_t* fd = nz && v > 4u ? &freq[v + 1u] : &junk32[t];
+                atomicAdd(fd, 1u);
+                hot += nz && v <= 4u ? 1ull << (16u * (v - 1u)) : 0ull;
+                pos += nz ? 1u : 0u;
+                z = nz ? 0u : z + 1u;
             }
-        };
-        z = carry;
-        each([&](uint32_t v) {
-            if (v != 0) {
-                if (z) zeros(z);
-                emit(v + 1);
+        }
+        // the digits, each run before the nonzero value ending it
+        {
+            uint32_t dsum = 0;  // digits of the runs ending before i
+            for (uint64_t r = R; r; r &= r - 1ull) {
+                const uint32_t i = (uint32_t)__builtin_ctzll(r), z = run_len(i);
+                digits(wr + (uint32_t)__popcll(NZ & ((1ull << i) - 1ull)) + dsum, z);
+                dsum += run_digits(z);
             }
-            z = v == 0 ? z + 1u : 0u;
-        });
+        }
         if (has_last) {
-            if (z) zeros(z);
-            emit(EOB);
+            if (zend) digits(wr + w - 1u - dend, zend);
+            tile_out[wr + w - 1u] = (uint16_t)EOB;
+            atomicAdd(&freq[EOB], 1u);
         }
         __syncthreads();
         const uint32_t base = s_wr;
@@ -2337,9 +2362,12 @@ __global__ __launch_bounds__(kRle2Threads) void rle2(Batch B)
         __syncthreads();
     }
     static_assert(kRunA == 0 && kRunB == 1, "RUNA / RUNB are symbols 0 and 1");
+    // wave sums of the register counters, one atomic per wave and symbol
+    uint32_t cnts[6] = {nrunA, nrunB, (uint32_t)(hot & 0xFFFFu), (uint32_t)((hot >> 16) & 0xFFFFu),
+                        (uint32_t)((hot >> 32) & 0xFFFFu), (uint32_t)(hot >> 48)};
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-        uint32_t c = r ? nrunB : nrunA;
+    for (int r = 0; r < 6; ++r) {
+        uint32_t c = cnts[r];
         for (int d = 32; d > 0; d >>= 1) c += (uint32_t)__shfl_xor((int)c, d);
         if (lane == 0 && c) atomicAdd(&freq[r], c);
     }
@@ -2426,6 +2454,7 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
 {
     __shared__ uint32_t rfreq[kMaxGroups][kMaxAlpha];
     __shared__ uint64_t lpack[kMaxAlpha + 1];
+    __shared__ uint32_t junk[kHuffThreads];
     const uint32_t s = blockIdx.x, t = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t nMTF = B.nmtf[s], nSel = B.nsel[s];
@@ -2468,12 +2497,22 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
             if (cq < bc) { bc = cq; bt = q; }
         }
         sel[g] = (uint8_t)bt;
+        // symbols 0 .. 3 (RUNA, RUNB and the two smallest values: most of
+        // them) counted in 8-bit fields, the others by LDS atomics (the hot
+        // bins' atomics serialised on bank conflicts); a lane's other symbols
+        // land in its own junk word
+        uint32_t hot = 0;
 #pragma unroll
         for (int q = 0; q < kGSize / 2; ++q) {
             const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
-            if (lo != (uint32_t)kMaxAlpha) atomicAdd(&rfreq[bt][lo], 1u);
-            if (hi != (uint32_t)kMaxAlpha) atomicAdd(&rfreq[bt][hi], 1u);
+            hot += lo < 4u ? 1u << (8u * lo) : 0u;
+            hot += hi < 4u ? 1u << (8u * hi) : 0u;
+            atomicAdd(lo >= 4u && lo != (uint32_t)kMaxAlpha ? &rfreq[bt][lo] : &junk[t], 1u);
+            atomicAdd(hi >= 4u && hi != (uint32_t)kMaxAlpha ? &rfreq[bt][hi] : &junk[t], 1u);
         }
+#pragma unroll
+        for (uint32_t f = 0; f < 4; ++f)
+            if ((hot >> (8u * f)) & 0xFFu) atomicAdd(&rfreq[bt][f], (hot >> (8u * f)) & 0xFFu);
     }
     __syncthreads();
     uint32_t* rf = B.rfreq + (size_t)s * kMaxGroups * kMaxAlpha;
@@ -3419,7 +3458,10 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     uint32_t covered = kKeyBytes;
     bool none_left = false;  // a count read 0 and no kernel ran since: skip the later reads
     uint32_t first_ties = 0, left_runs = 0;  // tied slots after the chunk sorts, runs tie_runs_direct left (LFM_BZ2_STATS)
-    for (B.it_full = 0;; B.it_full = 1) {
+#ifndef LFM_BWT_FORCE_FULL
+#define LFM_BWT_FORCE_FULL 0  // timing variants: every rotation sorted, no induction
+#endif
+    for (B.it_full = LFM_BWT_FORCE_FULL;; B.it_full = 1) {
         ChunkLists CL;
         const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
         for (int c = 0; c < 4; ++c) {
