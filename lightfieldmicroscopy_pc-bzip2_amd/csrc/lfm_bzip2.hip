@@ -625,10 +625,13 @@ struct ChunkLists {
 };
 
 // A tile of the text for the bucket pass: T[i0 - 1 .. i0 + m + 8) cyclically
-// in tile[0 .. m + 9), m = min(n - i0, kBktTile).  bucket_fetch loads this
+// in tile[kTOff - 1 .. kTOff + m + 8), m = min(n - i0, kBktTile) (T[i0 + k]
+// at tile[kTOff + k]: word-aligned stores).  bucket_fetch loads this
 // thread's part (4 bytes; one edge byte for threads 0..8) into registers, a
 // tile ahead of bucket_put, which stores it into LDS: the pass is a chain of
-// tiles, and waiting for each tile's loads was most of its time.
+// tiles, and waiting for each tile's loads was most of its time.  Tiles
+// alternate between two buffers, so one barrier per tile orders them.
+constexpr uint32_t kTOff = 4;
 struct BktPart {
     uint32_t w;
     uint32_t e;
@@ -655,17 +658,14 @@ __device__ __forceinline__ uint32_t bucket_put(const BktPart& p, uint32_t n, uin
 {
     const uint32_t t = threadIdx.x;
     const uint32_t m = min(n - i0, kBktTile);
-    if (4 * t < m) {
-        tile[1 + 4 * t] = (uint8_t)p.w;
-        tile[2 + 4 * t] = (uint8_t)(p.w >> 8);
-        tile[3 + 4 * t] = (uint8_t)(p.w >> 16);
-        tile[4 + 4 * t] = (uint8_t)(p.w >> 24);
+    if (4 * t + 4 <= m) {
+        *(uint32_t*)(tile + kTOff + 4 * t) = p.w;
+    } else if (4 * t < m) {  // the last partial word: its valid bytes only (the edge bytes follow)
+        for (uint32_t b = 0; b < m - 4 * t; ++b) tile[kTOff + 4 * t + b] = (uint8_t)(p.w >> (8 * b));
     }
-    __syncthreads();  // the edge bytes overwrite the bytes read past the tile
-    if (t < 8) tile[1 + m + t] = (uint8_t)p.e;
-    else if (t == 8) tile[0] = (uint8_t)p.e;
-    __syncthreads();
-    return m;
+    if (t < 8) tile[kTOff + m + t] = (uint8_t)p.e;
+    else if (t == 8) tile[kTOff - 1] = (uint8_t)p.e;
+    return m;  // the caller's barrier publishes the tile
 }
 
 // LDS slot of bucket `key` (BITS bits: the first byte, then the top BITS - 8
@@ -694,7 +694,7 @@ __device__ __forceinline__ uint32_t bkt_slot(uint32_t key)
 // the B ones (kModeSortA).  The pass sorts the A rotations unless the B ones
 // are clearly fewer: on 16-bit little-endian symbols the A rotations start at
 // the low bytes, whose first byte spreads them over the buckets, while the B
-// ones start at the (mostly zero) high bytes.  rot_type reads tile[1 + k + d]
+// ones start at the (mostly zero) high bytes.  rot_type reads tile[kTOff + k + d]
 // for d <= 8 (the tile holds 8 bytes past its end): 1 = B, 0 = A, 2 = still
 // undecided after 8 equal bytes (only runs of 0xFB survive RLE1 that long: the
 // stream is then sorted whole, kModeFull).
@@ -705,7 +705,7 @@ __device__ __forceinline__ uint32_t rot_type(const uint8_t* tile, uint32_t k, ui
     if (a != b) return a < b ? 1u : 0u;
 #pragma unroll 1
     for (uint32_t d = 1; d < 8; ++d) {
-        const uint32_t x = tile[1 + k + d], y = tile[2 + k + d];
+        const uint32_t x = tile[kTOff + k + d], y = tile[kTOff + 1 + k + d];
         if (x != y) return x < y ? 1u : 0u;
     }
     return 2u;
@@ -722,7 +722,7 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
 {
     constexpr uint32_t kBuckets = 1u << BITS;
     __shared__ uint32_t hist[kBuckets];  // 64 KiB at 14 bits
-    __shared__ uint8_t tile[kBktTile + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t tiles[2][kBktTile + 16];
     __shared__ uint32_t cuts[kMaxCuts];
     __shared__ uint32_t wsum[kBucketThreads / 64], wcut[kBucketThreads / 64];
     __shared__ uint32_t ccount[4], cbase[4];
@@ -746,20 +746,22 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
         if (t == 0) undecided = n_unsorted = 0;
         __syncthreads();
         BktPart nx = bucket_fetch(T, n, 0);
-        for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
+        for (uint32_t i0 = 0, it = 0; i0 < n; i0 += kBktTile, ++it) {
             const BktPart cur = nx;
             nx = bucket_fetch(T, n, i0 + kBktTile);
+            uint8_t* tile = tiles[it & 1];
             const uint32_t m = bucket_put(cur, n, i0, tile);
+            __syncthreads();
             for (uint32_t k = t; k < m; k += kBucketThreads) {
-                const uint32_t a = tile[1 + k], b = tile[2 + k];
+                const uint32_t a = tile[kTOff + k], b = tile[kTOff + 1 + k];
                 const uint32_t ty = mode == kModeFull ? 3u : rot_type(tile, k, a, b);
                 if (ty == 2u) undecided = 1u;
                 else if (mode == kModeFull || ty == (mode == kModeSortB ? 1u : 0u))
                     atomicAdd(&hist[bkt_slot<BITS>((a << (BITS - 8)) | (b >> (16 - BITS)))], 1u);
                 else atomicAdd(&cnt_u[a], 1u);
             }
-            __syncthreads();
         }
+        __syncthreads();
         if (mode == kModeFull) break;
         if (undecided) {
             mode = kModeFull;
@@ -877,19 +879,20 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
     // rebuild the 8-byte keys from the text (rot_key8_fast), which the L2s
     // hold, instead of 8-byte scattered key writes and their re-read
     BktPart nx = bucket_fetch(T, n, 0);
-    for (uint32_t i0 = 0; i0 < n; i0 += kBktTile) {
+    for (uint32_t i0 = 0, it = 0; i0 < n; i0 += kBktTile, ++it) {
         const BktPart cur = nx;
         nx = bucket_fetch(T, n, i0 + kBktTile);
+        uint8_t* tile = tiles[it & 1];
         const uint32_t m = bucket_put(cur, n, i0, tile);
+        __syncthreads();
         for (uint32_t k = t; k < m; k += kBucketThreads) {
-            const uint8_t* p = tile + 1 + k;
+            const uint8_t* p = tile + kTOff + k;
             const uint32_t a = p[0], b = p[1];
             if (rot_sorted(tile, k, a, b, mode)) {
                 const uint32_t pos = atomicAdd(&hist[bkt_slot<BITS>((a << (BITS - 8)) | (b >> (16 - BITS)))], 1u);
                 B.vals_a[o + pos] = (i0 + k) | ((uint32_t)p[-1] << 24);
             }
         }
-        __syncthreads();
     }
 }
 
