@@ -581,6 +581,39 @@ def rank_layout(gpus, env, ndev):
     return world, rank, local, int(env.get("LOCAL_WORLD_SIZE", str(world)))
 
 
+def predictor_standalone(d_img, zf, k, alg_bytes, launches=20):
+    """The roofline kernel with the GPU to itself: `launches` launches of the
+    config-3 predictor over the resident stack on one HIP stream, timed one by
+    one with HIP events on that stream.  "warm": back to back; "flushed": a
+    1 GiB device fill before each launch (on the same stream, outside its
+    events), so each launch starts with the caches holding someone else's
+    dirty lines, as in the encode."""
+    sym = torch.empty_like(d_img)
+    scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    out = {"launches": launches, "predictor": k, "algorithmic_bytes": alg_bytes}
+    with torch.cuda.stream(st):
+        for mode in ("warm", "flushed"):
+            ms = []
+            for i in range(launches + 2):
+                if mode == "flushed":
+                    scratch.fill_(i & 0xFF)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                lfm.predict_device(d_img, sym, X, Y, zf, T, FAMILY, k, stream=st)
+                e1.record(st)
+                e1.synchronize()
+                if i >= 2:
+                    ms.append(e0.elapsed_time(e1))
+            med = float(np.median(ms))
+            out[mode] = {"kernel_ms_median": round(med, 4), "kernel_ms_min": round(float(min(ms)), 4),
+                         "frac": round(alg_bytes / (med / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
+    st.synchronize()
+    del scratch, sym
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -792,6 +825,8 @@ def main():
                 line["inproc"] = inproc_leg(local, node_threads if backend == "nccl" else threads,
                                             [[local], devs])
             dist.barrier(group=cpu_group)
+    if rank == 0 and world == 1:
+        line["roofline"]["standalone"] = predictor_standalone(d_img, zf, int(stats[-1]["chosen"]) & 0x7F, alg_bytes)
     buf = bytes(b) if rank == 0 and world == 1 and not args.no_decode else None  # before b's buffer is reused
     if rank == 0 and world == 1 and not args.no_host_input:
         line["host_input"] = host_input_rates(enc, d_img, zf)
