@@ -2183,7 +2183,10 @@ __device__ __forceinline__ bool heap_narrow(const Batch& B, uint32_t s, int alph
     return B.nmtf[s] + (uint32_t)alphaSize < kNarrowWeight;
 }
 
-constexpr int kRle2Threads = 256;
+#ifndef LFM_RLE2_THREADS
+#define LFM_RLE2_THREADS 256
+#endif
+constexpr int kRle2Threads = LFM_RLE2_THREADS;
 constexpr uint32_t kRle2Per = 64;                        // m values per thread and tile
 constexpr uint32_t kRle2Tile = kRle2Threads * kRle2Per;  // 16384
 
@@ -3664,11 +3667,22 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
     mark(4);
+    // stage hook 3 once the Huffman tables are done (emission and compaction
+    // still queued): a caller may start its next work beside this tail
+    static thread_local hipEvent_t ev_tables = nullptr;
+    static thread_local int ev_tables_dev = -1;
+    if (t_hook && ev_tables_dev != dev) {
+        if (ev_tables) (void)hipEventDestroy(ev_tables);
+        ev_tables = nullptr;
+        if (hipEventCreateWithFlags(&ev_tables, hipEventDisableTiming) == hipSuccess) ev_tables_dev = dev;
+    }
+    const bool hook3 = t_hook && ev_tables && hipEventRecord(ev_tables, st) == hipSuccess;
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(1024), 0, st, B.out_bytes, count, offs);
     hipLaunchKernelGGL(compact_streams, dim3(count), dim3(256), 0, st, B, offs, (uint8_t*)d_payload);
     mark(5);
     if (!ok()) return LFM_HIP_ERUNTIME;
+    if (hook3 && hipEventSynchronize(ev_tables) == hipSuccess) t_hook(t_hook_ctx, 3);
     static const bool stats = std::getenv("LFM_BZ2_STATS") && std::atoi(std::getenv("LFM_BZ2_STATS")) != 0;
     if (stats) {
         uint32_t c[8] = {};

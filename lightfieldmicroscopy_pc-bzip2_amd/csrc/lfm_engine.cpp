@@ -1304,9 +1304,33 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                 cv.notify_all();
                 break;
             }
+            // the slot's last batch releases the next encode once its Huffman
+            // tables are done (stage hook 3), so the next encode's first
+            // kernels queue while this one's emission and copies finish
+            const bool last = fly && b + nslots >= nbatch;
+            struct ReachOnce {
+                Inflight* f;
+                bool done;
+            } ro{fly, false};
+            // (measured +2.6 % end to end against the release after the
+            // batch's last copy: the ~0.45 ms host turnaround between two
+            // encodes' kernels is hidden, profiles/r05_ab_early_release.jsonl)
+            if (last)
+                lfm_hip_bzip2_set_stage_hook(
+                    [](void* c, int stage) {
+                        auto* r = (ReachOnce*)c;
+                        if (stage == 3 && !r->done) {
+                            r->done = true;
+                            r->f->reach();
+                        }
+                    },
+                    &ro);
             int ok = lfm_hip_bzip2_blocks(d_sym, dims, bs, (uint32_t)bpp, (uint32_t)b0, cnt, (uint32_t)level, sl.d_ws,
                                           ws, sl.d_out, sizes[b].data(), flags[b].data(), sl.stream) == LFM_HIP_OK;
-            if (fly && b + nslots >= nbatch) fly->reach();
+            if (last) {
+                lfm_hip_bzip2_set_stage_hook(nullptr, nullptr);
+                if (!ro.done) fly->reach();
+            }
             float sm[5];
             if (ok && lfm_hip_bzip2_last_stage_ms(sm) == 0)
                 for (int i = 0; i < 5; ++i) stage_ms[k][i] += sm[i];
