@@ -3656,6 +3656,17 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     mark(3);
     if (t_hook) t_hook(t_hook_ctx, 2);  // after the wide-stream count's synchronisation: rle2 has run
     hipLaunchKernelGGL(huff_init, dim3(count), dim3(64), 0, st, B);
+    // stage hook 3 once the Huffman tables are done (emission and compaction
+    // still queued): a caller may start its next work beside this tail
+    // (earlier, after the second or third code-length round, measured slower:
+    // the next encode's kernels then slow these latency-bound rounds)
+    static thread_local hipEvent_t ev_tables = nullptr;
+    static thread_local int ev_tables_dev = -1;
+    if (t_hook && ev_tables_dev != dev) {
+        if (ev_tables) (void)hipEventDestroy(ev_tables);
+        ev_tables = nullptr;
+        if (hipEventCreateWithFlags(&ev_tables, hipEventDisableTiming) == hipSuccess) ev_tables_dev = dev;
+    }
     for (int it = 0; it < kIters; ++it) {
         hipLaunchKernelGGL(huff_select_reg, dim3(count), dim3(kHuffThreads), 0, st, B);
         // uniform heaps, 32 per workgroup: u32 entries for the narrow tables,
@@ -3667,15 +3678,6 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     }
     hipLaunchKernelGGL(huff_final, dim3(count), dim3(64), 0, st, B);
     mark(4);
-    // stage hook 3 once the Huffman tables are done (emission and compaction
-    // still queued): a caller may start its next work beside this tail
-    static thread_local hipEvent_t ev_tables = nullptr;
-    static thread_local int ev_tables_dev = -1;
-    if (t_hook && ev_tables_dev != dev) {
-        if (ev_tables) (void)hipEventDestroy(ev_tables);
-        ev_tables = nullptr;
-        if (hipEventCreateWithFlags(&ev_tables, hipEventDisableTiming) == hipSuccess) ev_tables_dev = dev;
-    }
     const bool hook3 = t_hook && ev_tables && hipEventRecord(ev_tables, st) == hipSuccess;
     hipLaunchKernelGGL(emit_stream, dim3(count), dim3(kEmitThreads), 0, st, B);
     hipLaunchKernelGGL(scan_offsets, dim3(1), dim3(1024), 0, st, B.out_bytes, count, offs);
