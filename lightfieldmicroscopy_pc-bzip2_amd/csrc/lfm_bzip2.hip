@@ -606,7 +606,10 @@ constexpr uint32_t kBucketBits = 14;               // 64 KiB histogram, two work
                                                    // buckets overflow the small sorter)
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
-constexpr uint32_t kChunk = 1024;
+#ifndef LFM_CHUNK
+#define LFM_CHUNK 1024
+#endif
+constexpr uint32_t kChunk = LFM_CHUNK;
 constexpr int kCsThreads = 512, kCsItems = 4;      // chunks up to 2 048 (every multi-bucket chunk); 512 x 4 measured
                                                    // 10 % faster than 256 x 8
 constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
@@ -1442,6 +1445,23 @@ __global__ __launch_bounds__(256) void bwt_flag_periodic(Batch B, const uint32_t
         atomicOr(&B.flags[cl[c] / B.cap], kFlagHost);
 }
 
+__device__ __forceinline__ void make_u2s(const Batch& B, uint32_t s, uint8_t* u2s, uint32_t lane, uint32_t* nin_out)
+{
+    uint32_t inu[8], nin = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        inu[q] = B.inuse[s * 8 + q];
+        nin += __popc(inu[q]);
+    }
+    for (uint32_t c = lane; c < 256; c += 64) {
+        uint32_t below = 0;
+        for (uint32_t q = 0; q < (c >> 5); ++q) below += __popc(inu[q]);
+        below += __popc(inu[c >> 5] & ((1u << (c & 31)) - 1u));
+        u2s[c] = (uint8_t)below;
+    }
+    *nin_out = nin;
+}
+
 // ------------------------------------------------------------ induction --
 // bwt_place_sorted + bwt_induce: the final order from the sorted rotations.
 // In the final order (position q) bucket c (first byte c) holds its A
@@ -1507,15 +1527,20 @@ __device__ __forceinline__ void ind_tables(const Batch& B, uint32_t s, uint32_t 
 __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks)
 {
     __shared__ uint32_t q0[256], p0[256], p1[256], s0[256], wtmp[8];
+    __shared__ uint8_t u2s[256];
     const uint32_t t = threadIdx.x, k = blockIdx.x >> 3;
     const uint32_t s = (blockIdx.x & 7u) + 8u * (k / chunks), base = (k % chunks) * kPlaceChunk;
     if (s >= B.nstreams || (B.flags[s] & kFlagHost)) return;
     const uint32_t n = B.n[s], ns = B.nsub[s], mode = B.bwt_mode[s];
     if (base >= n) return;
-    ind_tables(B, s, mode, q0, p0, p1, s0, wtmp);
+    if (mode == kModeFull && t < 64) {
+        uint32_t nin;
+        make_u2s(B, s, u2s, t, &nin);
+    }
+    ind_tables(B, s, mode, q0, p0, p1, s0, wtmp);  // (its barriers publish u2s)
     const size_t o = (size_t)s * B.cap;
     const uint8_t* T = B.T + o;
-    uint32_t* SF = B.sfin + o;
+    uint8_t* LL = (uint8_t*)B.mtfv + o;  // the BWT output symbols (mtf_last<true> and mtf_win read them)
     uint2* E = B.ent + o;
     // the sorted slots [base, base + kPlaceChunk): sa, then T[i-4 .. i], all
     // loads issued before any is used
@@ -1548,8 +1573,10 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks
             c = T[i];
         }
         const uint32_t qq = (mode == kModeSortA ? q0[c] : p1[c]) + (j - s0[c]);
-        if (mode == kModeFull)
-            SF[qq] = v[q];  // the final order already
+        if (mode == kModeFull) {  // the final order already: the symbol, and origPtr at rotation 0
+            LL[qq] = u2s[v[q] >> 24];
+            if (i == 0) B.orig_ptr[s] = qq;
+        }
         else
             E[qq] = make_uint2(v[q] | (3u << 20),
                                ((x >> 16) & 0xFFu) | (((x >> 8) & 0xFFu) << 8) | ((x & 0xFFu) << 16) | (c << 24));
@@ -1615,7 +1642,8 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
     __shared__ uint32_t head[256];            // next free scan position of bucket u's placed part
     __shared__ uint2 ring[kIndRing];
     __shared__ __attribute__((aligned(16))) uint2 stg[kIndBlock + 32];      // the next block's entries, in q order
-    __shared__ __attribute__((aligned(16))) uint32_t fin[kIndBlock + 256];  // the block's final values, in q order
+    __shared__ __attribute__((aligned(16))) uint8_t fin[kIndBlock + 32];  // the block's symbols, in q order
+    __shared__ uint8_t u2s[256];
     const uint32_t s = blockIdx.x, lane = threadIdx.x;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
@@ -1624,9 +1652,12 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
     const bool rev = mode == kModeSortA;      // right to left, mirrored bytes
     const uint32_t mir = rev ? 255u : 0u;
     const size_t o = (size_t)s * B.cap;
-    uint32_t* SF = B.sfin + o;
+    uint8_t* LL = (uint8_t*)B.mtfv + o;  // the BWT output symbols (mtf_last<true> and mtf_win read them)
     uint2* E = B.ent + o;
     const uint8_t* T = B.T + o;
+    uint32_t nin;
+    make_u2s(B, s, u2s, lane, &nin);
+    const bool u2s_id = nin == 256;  // every byte in use: the map is the identity
     {  // head[u] = scan-order start of bucket u (its placed part comes first)
         uint32_t nt[4], l = 0;
 #pragma unroll
@@ -1648,9 +1679,9 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
         }
     }
     for (uint32_t i = lane; i < kIndRing; i += 64) ring[i].x = kIndPend;
-    // position in `ent` / sfin of scan position v.  A block [vb, vb + kIndBlock)
+    // position in `ent` / ll of scan position v.  A block [vb, vb + kIndBlock)
     // covers q in [qwin(vb), qwin(vb) + kIndBlock); stg holds it from q =
-    // qwin & ~1, fin from q = qwin & ~3 (16-byte aligned transfers)
+    // qwin & ~1, fin from q = qwin & ~15 (16-byte aligned transfers)
     const uint32_t qa = rev ? n - 1 : 0u;
     auto qof = [&](uint32_t v) { return rev ? qa - v : v; };
     auto qwin = [&](uint32_t vb) { return rev ? (int)n - (int)kIndBlock - (int)vb : (int)vb; };
@@ -1682,20 +1713,29 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
             if (v < n && x[k].x != kIndPend) ring[v % kIndRing] = x[k];
         }
     };
-    auto flush = [&](uint32_t vb) {  // the block's final values to sfin, 16 bytes per lane
-        const int qw = qwin(vb), qf = qw & ~3;
+    auto flush = [&](uint32_t vb) {  // the block's symbols to ll, 16 bytes per lane
+        const int qw = qwin(vb), qf = qw & ~15;
         const int lo = max(qw, 0), hi = min(qw + (int)kIndBlock, (int)n);  // the block's positions
-        for (uint32_t j = 0; j < (kIndBlock + 256) / 256 && (int)(256 * j) < hi - qf; ++j) {
-            const uint32_t w = 256 * j + 4 * lane;
-            const uint4 f = *(const uint4*)&fin[w];
+        const uint32_t w = 16 * lane;
+        if (w < kIndBlock + 32 && (int)w < hi - qf) {
+            uint4 f = *(const uint4*)&fin[w];  // the bytes before each rotation, mapped to symbols here
+            if (!u2s_id) {
+                uint32_t* fw = &f.x;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t x = fw[r];
+                    fw[r] = (uint32_t)u2s[x & 255u] | ((uint32_t)u2s[(x >> 8) & 255u] << 8) |
+                            ((uint32_t)u2s[(x >> 16) & 255u] << 16) | ((uint32_t)u2s[x >> 24] << 24);
+                }
+            }
             const int q = qf + (int)w;
-            if (q >= lo && q + 3 < hi) {
-                *(uint4*)(SF + q) = f;
+            if (q >= lo && q + 15 < hi) {
+                *(uint4*)(LL + q) = f;
             } else {
                 const uint32_t fv[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if (q + r >= lo && q + r < hi) SF[q + r] = fv[r];
+                for (int r = 0; r < 16; ++r)
+                    if (q + r >= lo && q + r < hi) LL[q + r] = (uint8_t)(fv[r >> 2] >> (8 * (r & 3)));
             }
         }
     };
@@ -1710,6 +1750,7 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
 #define IND_T(x) do { } while (0)
 #endif
     bool bad = false;  // inconsistent counts or a pending entry no earlier lane places (never)
+    uint32_t org = ~0u;
     for (uint32_t v0 = 0; v0 < n && !bad; v0 += kIndBlock) {
 #if LFM_IND_PROF
         pt0 = clock64();
@@ -1775,7 +1816,8 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                     b[k] = (lo >> 24) ^ mir;
                     const uint32_t u = (hi >> 24) ^ mir;
                     ind[k] = me && (b[k] > u || (b[k] == u && (lo & kIndPlaced)));
-                    if (me) fin[wof(vs - v0 + 64 * k + lane, qwin(v0) & 3)] = lo & ~(0xFu << 20);
+                    if (me) fin[wof(vs - v0 + 64 * k + lane, qwin(v0) & 15)] = (uint8_t)(lo >> 24);
+                    org = me && (lo & kIndIdx) == 0 ? qof(vs + 64 * k + lane) : org;  // origPtr: rotation 0
                     rem[k] = __ballot(ind[k]);
                     left |= rem[k];
                 }
@@ -1892,6 +1934,7 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
 #endif
 #undef IND_T
     if (bad && lane == 0) B.flags[s] |= kFlagHost;  // the host library redoes the stream
+    if (org != ~0u) B.orig_ptr[s] = org;
 }
 
 // ------------------------------------------------------------------ MTF --
@@ -1911,23 +1954,10 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
 //               chunks by a scan, as in rle1_crc)
 constexpr uint32_t kSeg = 4096;
 
-__device__ __forceinline__ void make_u2s(const Batch& B, uint32_t s, uint8_t* u2s, uint32_t lane, uint32_t* nin_out)
-{
-    uint32_t inu[8], nin = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        inu[q] = B.inuse[s * 8 + q];
-        nin += __popc(inu[q]);
-    }
-    for (uint32_t c = lane; c < 256; c += 64) {
-        uint32_t below = 0;
-        for (uint32_t q = 0; q < (c >> 5); ++q) below += __popc(inu[q]);
-        below += __popc(inu[c >> 5] & ((1u << (c & 31)) - 1u));
-        u2s[c] = (uint8_t)below;
-    }
-    *nin_out = nin;
-}
 
+// FROM_LL: bwt_place_sorted / bwt_induce already wrote the symbols ll[] (and
+// origPtr); else (a batch sorted whole) they come from sa here
+template <bool FROM_LL>
 __global__ __launch_bounds__(256) void mtf_last(Batch B, uint32_t nseg_max, int32_t* __restrict__ seg_last)
 {
     __shared__ uint8_t u2s[4][256];
@@ -1949,24 +1979,34 @@ __global__ __launch_bounds__(256) void mtf_last(Batch B, uint32_t nseg_max, int3
     // of the symbols), loaded an iteration ahead at a clamped, aligned index
     // (sa holds cap >= n + 8 entries per stream)
     const uint32_t jlast = (j1 - 1) & ~3u;
-    uint4 vn = *(const uint4*)(B.sa + o + min(j0 + 4 * lane, jlast));
+    uint4 vn;
+    uint32_t wn = 0;
+    if constexpr (FROM_LL) wn = *(const uint32_t*)(llbuf + min(j0 + 4 * lane, jlast));
+    else vn = *(const uint4*)(B.sa + o + min(j0 + 4 * lane, jlast));
     for (uint32_t jb = j0; jb < j1; jb += 256) {
         const uint32_t j = jb + 4 * lane;
-        const uint4 v4 = vn;
-        vn = *(const uint4*)(B.sa + o + min(j + 256, jlast));
-        const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
         uint32_t ll[4];
+        if constexpr (FROM_LL) {
+            const uint32_t w4 = wn;
+            wn = *(const uint32_t*)(llbuf + min(j + 256, jlast));
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            ll[q] = u2s[wave][v[q] >> 24];
-            if (j + q < j1 && (v[q] & kIdxMask) == 0) B.orig_ptr[s] = j + q;  // BZ2_blockSort: origPtr = sorted position of rotation 0
-        }
-        if (j + 3 < j1) {
-            *(uint32_t*)(llbuf + j) = ll[0] | (ll[1] << 8) | (ll[2] << 16) | (ll[3] << 24);
+            for (uint32_t q = 0; q < 4; ++q) ll[q] = (w4 >> (8 * q)) & 0xFFu;
         } else {
+            const uint4 v4 = vn;
+            vn = *(const uint4*)(B.sa + o + min(j + 256, jlast));
+            const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                if (j + q < j1) llbuf[j + q] = (uint8_t)ll[q];
+            for (uint32_t q = 0; q < 4; ++q) {
+                ll[q] = u2s[wave][v[q] >> 24];
+                if (j + q < j1 && (v[q] & kIdxMask) == 0) B.orig_ptr[s] = j + q;  // BZ2_blockSort: origPtr = sorted position of rotation 0
+            }
+            if (j + 3 < j1) {
+                *(uint32_t*)(llbuf + j) = ll[0] | (ll[1] << 8) | (ll[2] << 16) | (ll[3] << 24);
+            } else {
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    if (j + q < j1) llbuf[j + q] = (uint8_t)ll[q];
+            }
         }
         // only the last position of each run of equal symbols can be the
         // symbol's last: the BWT output is runs, and 64 lanes on one LDS word
@@ -3643,7 +3683,8 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         const uint32_t nseg_max = (B.cap + kSeg - 1) / kSeg;
         int32_t* seg_last = (int32_t*)B.keys_a;  // free after the BWT (count * nseg_max KiB << N * 8 bytes)
         const dim3 g((nseg_max + 3) / 4, count);
-        hipLaunchKernelGGL(mtf_last, g, dim3(256), 0, st, B, nseg_max, seg_last);
+        if (B.it_full) hipLaunchKernelGGL(mtf_last<false>, g, dim3(256), 0, st, B, nseg_max, seg_last);
+        else hipLaunchKernelGGL(mtf_last<true>, g, dim3(256), 0, st, B, nseg_max, seg_last);
         hipLaunchKernelGGL(mtf_prefix, dim3(count), dim3(256), 0, st, B, nseg_max, seg_last);
         hipLaunchKernelGGL(mtf_win, g, dim3(256), 0, st, B, nseg_max, (const int32_t*)seg_last);
         hipLaunchKernelGGL(rle2, dim3(count), dim3(kRle2Threads), 0, st, B);
