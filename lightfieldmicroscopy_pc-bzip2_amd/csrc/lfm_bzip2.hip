@@ -133,6 +133,7 @@ struct Batch {
     uint32_t* nsub;          // rotations sorted per stream (the A or B rotations, or all of them)
     uint32_t* bwt_mode;      // per stream: kModeSortA / kModeSortB / kModeFull
     uint32_t* abcnt;         // per stream: A rotations per first byte [256], then B rotations [256]
+    uint32_t* itab;          // per stream: q0, p0, p1, s0 [256] each (bwt_bucket, for bwt_place_sorted)
     uint32_t* sfin;          // the final order of every rotation (bwt_place_sorted / bwt_induce)
     uint2* ent;              // bwt_induce's entries per final position (the keys_a area, free after the sorts)
     uint32_t it_full;        // sort every rotation (no induction): the fallback for ties that need doubling
@@ -732,6 +733,7 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
     __shared__ uint32_t sinuse[8];                  // bytes present in the RLE1 text (the stream's inUse map)
     __shared__ uint32_t cnt_u[256], cnt_s[256];     // unsorted / sorted rotations per first byte
     __shared__ uint32_t undecided, n_unsorted;
+    __shared__ uint32_t tsum[8];
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
     const uint32_t n = B.n[s];
@@ -842,9 +844,43 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
         });
     }
     if (t < 8) B.inuse[s * 8 + t] = sinuse[t];  // (written after the scan's barrier)
-    if (t < 256) {  // A / B rotations per first byte for bwt_induce
-        B.abcnt[(size_t)s * 512 + t] = mode == kModeSortA ? cnt_s[t] : cnt_u[t];
-        B.abcnt[(size_t)s * 512 + 256 + t] = mode == kModeSortA ? cnt_u[t] : cnt_s[t];
+    {  // A / B rotations per first byte for bwt_induce, and bwt_place_sorted's
+       // tables: q-order start of bucket c (q0), its placed part (p0 .. p1)
+       // and the first sa slot of its sorted rotations (s0)
+        uint32_t na = 0, nb = 0, ns = 0, x = 0, y = 0;
+        if (t < 256) {
+            na = mode == kModeSortA ? cnt_s[t] : cnt_u[t];
+            nb = mode == kModeSortA ? cnt_u[t] : cnt_s[t];
+            ns = mode == kModeSortA ? na : nb;  // (kModeFull: all in the B counts)
+            B.abcnt[(size_t)s * 512 + t] = na;
+            B.abcnt[(size_t)s * 512 + 256 + t] = nb;
+            x = na + nb;
+            y = ns;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t a = __shfl_up(x, d), b = __shfl_up(y, d);
+                if ((int)lane >= d) {
+                    x += a;
+                    y += b;
+                }
+            }
+            if (lane == 63) {
+                tsum[wave] = x;
+                tsum[4 + wave] = y;
+            }
+        }
+        __syncthreads();
+        if (t < 256) {
+            for (uint32_t w = 0; w < wave; ++w) {
+                x += tsum[w];
+                y += tsum[4 + w];
+            }
+            const uint32_t qs = x - na - nb;
+            uint32_t* it = B.itab + (size_t)s * 1024;
+            it[t] = qs;
+            it[256 + t] = mode == kModeSortA ? qs + na : qs;
+            it[512 + t] = mode == kModeSortA ? qs + na + nb : (mode == kModeSortB ? qs + na : qs);
+            it[768 + t] = y - ns;
+        }
     }
     if (t == 0) {
         B.nsub[s] = nsub;
@@ -1486,47 +1522,13 @@ constexpr uint32_t kIndIdx = 0xFFFFFu;      // n < nblock_max < 2^20
 constexpr uint32_t kIndPlaced = 1u << 23;
 constexpr uint32_t kPlaceChunk = 2048;  // sorted slots / positions per bwt_place_sorted workgroup
 
-// q-order starts of each bucket (q0[c]), its placed part (p0[c], p1[c]) and
-// the first sa slot of its sorted rotations (s0[c]), 256 threads
-__device__ __forceinline__ void ind_tables(const Batch& B, uint32_t s, uint32_t mode, uint32_t* q0, uint32_t* p0,
-                                           uint32_t* p1, uint32_t* s0, uint32_t* wtmp)
-{
-    const uint32_t c = threadIdx.x, lane = c & 63, wave = c >> 6;
-    const uint32_t na = B.abcnt[(size_t)s * 512 + c], nb = B.abcnt[(size_t)s * 512 + 256 + c];
-    const uint32_t ns = mode == kModeSortA ? na : nb;  // sorted (kModeFull: all in the B counts)
-    uint32_t x = na + nb, y = ns;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t a = __shfl_up(x, d), b = __shfl_up(y, d);
-        if ((int)lane >= d) {
-            x += a;
-            y += b;
-        }
-    }
-    if (lane == 63) {
-        wtmp[wave] = x;
-        wtmp[4 + wave] = y;
-    }
-    __syncthreads();
-    for (uint32_t w = 0; w < wave; ++w) {
-        x += wtmp[w];
-        y += wtmp[4 + w];
-    }
-    const uint32_t qs = x - na - nb;
-    q0[c] = qs;
-    s0[c] = y - ns;
-    // placed part: the A rotations (kModeSortB), the B ones (kModeSortA), none (kModeFull)
-    p0[c] = mode == kModeSortA ? qs + na : qs;
-    p1[c] = mode == kModeSortA ? qs + na + nb : (mode == kModeSortB ? qs + na : qs);
-    __syncthreads();
-}
-
 // One workgroup per kPlaceChunk sorted slots and final positions of a
 // stream, the chunks of a stream consecutive on one XCD (workgroup w runs on
 // XCD w % 8): the text reads are random inside the stream, so a stream's text
 // should stay in one L2 while its chunks run.
 __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks)
 {
-    __shared__ uint32_t q0[256], p0[256], p1[256], s0[256], wtmp[8];
+    __shared__ uint32_t q0[256], p0[256], p1[256], s0[256];
     __shared__ uint8_t u2s[256];
     const uint32_t t = threadIdx.x, k = blockIdx.x >> 3;
     const uint32_t s = (blockIdx.x & 7u) + 8u * (k / chunks), base = (k % chunks) * kPlaceChunk;
@@ -1537,7 +1539,14 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks
         uint32_t nin;
         make_u2s(B, s, u2s, t, &nin);
     }
-    ind_tables(B, s, mode, q0, p0, p1, s0, wtmp);  // (its barriers publish u2s)
+    {
+        const uint32_t* it = B.itab + (size_t)s * 1024;
+        q0[t] = it[t];
+        p0[t] = it[256 + t];
+        p1[t] = it[512 + t];
+        s0[t] = it[768 + t];
+    }
+    __syncthreads();
     const size_t o = (size_t)s * B.cap;
     const uint8_t* T = B.T + o;
     uint8_t* LL = (uint8_t*)B.mtfv + o;  // the BWT output symbols (mtf_last<true> and mtf_win read them)
@@ -3386,6 +3395,7 @@ extern "C" size_t lfm_hip_bzip2_workspace_bytes(uint32_t nstreams, uint32_t raw_
     b += align_up((size_t)nstreams * 8 * 4, 256);               // inuse
     b += align_up((size_t)nstreams * kMaxGroups * 4 + 64, 256);  // wide heap list
     b += align_up((size_t)nstreams * 512 * 4, 256);             // A / B rotations per first byte
+    b += align_up((size_t)nstreams * 1024 * 4, 256);            // placement tables
     b += 16 * align_up((size_t)nstreams * 4 + 64, 256);         // small per-stream arrays
     b += align_up(((size_t)nstreams + 1) * 8 + 32, 256);        // offsets + counters
     b += align_up(prim_tmp_bytes(nstreams, cap), 256);          // rocPRIM temporary storage
@@ -3465,6 +3475,7 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     B.inuse = (uint32_t*)take((size_t)count * 8 * 4);
     B.wide = (uint32_t*)take((size_t)count * kMaxGroups * 4 + 64);
     B.abcnt = (uint32_t*)take((size_t)count * 512 * 4);
+    B.itab = (uint32_t*)take((size_t)count * 1024 * 4);
     uint32_t** small[] = {&B.raw_len, &B.n, &B.crc, &B.flags, &B.done, &B.seg_begin, &B.seg_end, &B.nmtf,
                           &B.orig_ptr, &B.nsel, &B.ngroups, &B.out_bytes, &B.nsub, &B.bwt_mode};
     for (uint32_t** q : small) *q = (uint32_t*)take((size_t)count * 4 + 64);
