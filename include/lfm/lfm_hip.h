@@ -87,8 +87,10 @@ int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], const uint32
 int lfm_hip_bzip2_last_stage_ms(float ms[5]);
 /* Progress hook of the calling thread's lfm_hip_bzip2_blocks calls: fn(ctx,
  * stage) once the device has finished stage 1 (BWT) and stage 2 (MTF + RUNA/
- * RUNB), i.e. at the host synchronisations that follow them; fn == NULL
- * removes it.  The pipelined encoder starts the next stack's kernels there. */
+ * RUNB), at the host synchronisations that follow them, and stage 3 (the
+ * Huffman tables; emission and compaction still queued behind them); fn ==
+ * NULL removes it.  The pipelined encoder releases the next stack's GPU
+ * bzip2 at stage 3 of each slot's last batch. */
 void lfm_hip_bzip2_set_stage_hook(void (*fn)(void* ctx, int stage), void* ctx);
 
 /* GPU bzip2 decode of `count` single-block streams (the .lfm block payloads,

@@ -607,10 +607,7 @@ constexpr uint32_t kBucketBits = 14;               // 64 KiB histogram, two work
                                                    // buckets overflow the small sorter)
 constexpr int kBucketThreads = 1024;
 constexpr uint32_t kBktTile = 4096;
-#ifndef LFM_CHUNK
-#define LFM_CHUNK 1024
-#endif
-constexpr uint32_t kChunk = LFM_CHUNK;
+constexpr uint32_t kChunk = 1024;  // (512 equal, 2 048 slower end to end in round 5)
 constexpr int kCsThreads = 512, kCsItems = 4;      // chunks up to 2 048 (every multi-bucket chunk); 512 x 4 measured
                                                    // 10 % faster than 256 x 8
 constexpr int kBigThreads = 512, kBigItems = 8;    // single buckets up to 4 096
@@ -1071,12 +1068,7 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
     if (c >= nch) return;
     static_assert(IPT == 2 || IPT == 4 || IPT == 8, "flags are packed 2, 4 or 8 per thread");
-#ifndef LFM_CS_BITONIC
-#define LFM_CS_BITONIC 0
-#endif
-    using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t,
-                                     LFM_CS_BITONIC ? rocprim::block_sort_algorithm::bitonic_sort
-                                                    : rocprim::block_sort_algorithm::merge_sort>;
+    using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
     using ExK = rocprim::block_exchange<uint64_t, TH, IPT>;
     using ExV = rocprim::block_exchange<uint32_t, TH, IPT>;
     constexpr uint32_t NI = TH * IPT;
@@ -1130,8 +1122,7 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     __syncthreads();
     ExV().striped_to_blocked(v, v, sm.ev);
     __syncthreads();
-    if constexpr (LFM_CS_BITONIC) Sort().sort(k, v, sm.s);  // the padding keys (~0, never a text prefix) sort last
-    else Sort().sort(k, v, sm.s, m);
+    Sort().sort(k, v, sm.s, m);
     __syncthreads();
     sm.x.first[t] = k[0];
     sm.x.last[t] = k[IPT - 1];
@@ -1619,10 +1610,7 @@ __global__ __launch_bounds__(256) void bwt_place_sorted(Batch B, uint32_t chunks
 // in rounds up to its first pending lane.
 constexpr uint32_t kIndSlices = 8;
 constexpr uint32_t kIndBlock = 64 * kIndSlices;
-#ifndef LFM_IND_KS
-#define LFM_IND_KS 4
-#endif
-constexpr int kIndStepSlices = LFM_IND_KS;  // slices scanned together (one round of ballots and LDS latencies)
+constexpr int kIndStepSlices = 4;  // slices scanned together (2 and 8 measured slower in the pipeline)
 constexpr uint32_t kIndRing = 2 * kIndBlock;
 
 // LDS-DMA of 16 bytes per lane into LDS at `lds` + 16 * lane, from L2 (sc1:
@@ -2232,10 +2220,7 @@ __device__ __forceinline__ bool heap_narrow(const Batch& B, uint32_t s, int alph
     return B.nmtf[s] + (uint32_t)alphaSize < kNarrowWeight;
 }
 
-#ifndef LFM_RLE2_THREADS
-#define LFM_RLE2_THREADS 256
-#endif
-constexpr int kRle2Threads = LFM_RLE2_THREADS;
+constexpr int kRle2Threads = 256;  // (512 and 1 024 measured slower)
 constexpr uint32_t kRle2Per = 64;                        // m values per thread and tile
 constexpr uint32_t kRle2Tile = kRle2Threads * kRle2Per;  // 16384
 
@@ -2261,10 +2246,7 @@ __device__ __forceinline__ uint64_t zero_byte_mask64(const uint32_t (&q)[kRle2Pe
     return Z;
 }
 
-#ifndef LFM_RLE2_WPE
-#define LFM_RLE2_WPE 4
-#endif
-__global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(LFM_RLE2_WPE))) void rle2(Batch B)
+__global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4))) void rle2(Batch B)
 {
     constexpr uint32_t NW = kRle2Threads / 64;
     __shared__ uint32_t wz[NW], wa[NW], wc[NW];  // per-wave scan totals
