@@ -1511,7 +1511,7 @@ __device__ __forceinline__ void make_u2s(const Batch& B, uint32_t s, uint8_t* u2
 constexpr uint32_t kIndPend = 0xFFFFFFFFu;  // never an entry: nprev <= 3
 constexpr uint32_t kIndIdx = 0xFFFFFu;      // n < nblock_max < 2^20
 constexpr uint32_t kIndPlaced = 1u << 23;
-constexpr uint32_t kPlaceChunk = 2048;  // sorted slots / positions per bwt_place_sorted workgroup
+constexpr uint32_t kPlaceChunk = 2048;  // (1 024, 4 096, 8 192 equal or slower end to end)  // sorted slots / positions per bwt_place_sorted workgroup
 
 // One workgroup per kPlaceChunk sorted slots and final positions of a
 // stream, the chunks of a stream consecutive on one XCD (workgroup w runs on
