@@ -2250,10 +2250,9 @@ __global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4)
 {
     constexpr uint32_t NW = kRle2Threads / 64;
     __shared__ uint32_t wz[NW], wa[NW], wc[NW];  // per-wave scan totals
-    __shared__ uint32_t freq[kMaxAlpha];
-    __shared__ uint32_t junk32[kRle2Threads];
-    __shared__ uint16_t tile_out[kRle2Tile + 64];
-    __shared__ uint16_t junk16[kRle2Threads];
+    // freq[kMaxAlpha + t] and tile_out[kRle2Tile + 64 + t]: thread t's junk slots
+    __shared__ uint32_t freq[kMaxAlpha + kRle2Threads];
+    __shared__ uint16_t tile_out[kRle2Tile + 64 + kRle2Threads];
     __shared__ uint32_t s_carry, s_wr;
     const uint32_t s = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     if (B.flags[s] & kFlagHost) return;
@@ -2365,10 +2364,8 @@ __global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4)
                 const uint32_t v = (q[i >> 2] >> (8 * (i & 3))) & 0xFFu;
                 const bool nz = (NZ >> i) & 1u;
                 pos += nz && z ? run_digits(z) : 0u;
-                uint16_t* dst = nz ? &tile_out[pos] : &junk16[t];
-                *dst = (uint16_t)(v + 1u);
-                uint32_t* fd = nz && v > 4u ? &freq[v + 1u] : &junk32[t];
-                atomicAdd(fd, 1u);
+                tile_out[nz ? pos : kRle2Tile + 64 + t] = (uint16_t)(v + 1u);
+                atomicAdd(&freq[nz && v > 4u ? v + 1u : kMaxAlpha + t], 1u);
                 hot += nz && v <= 4u ? 1ull << (16u * (v - 1u)) : 0ull;
                 pos += nz ? 1u : 0u;
                 z = nz ? 0u : z + 1u;
