@@ -587,12 +587,17 @@ def predictor_standalone(d_img, zf, k, alg_bytes, launches=20):
     one with HIP events on that stream.  "warm": back to back; "flushed": a
     1 GiB device fill before each launch (on the same stream, outside its
     events), so each launch starts with the caches holding someone else's
-    dirty lines, as in the encode."""
+    dirty lines, as in the encode.  "copies": the same two protocols for plain
+    copies of the same bytes (the stack read once, as many bytes written) on
+    the same box -- the ceiling a streaming kernel of this traffic reaches
+    here: hipMemcpyAsync device to device and torch's elementwise add."""
     sym = torch.empty_like(d_img)
     scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
     st = torch.cuda.Stream()
     out = {"launches": launches, "predictor": k, "algorithmic_bytes": alg_bytes}
-    with torch.cuda.stream(st):
+
+    def timed(fn):
+        res = {}
         for mode in ("warm", "flushed"):
             ms = []
             for i in range(launches + 2):
@@ -600,15 +605,24 @@ def predictor_standalone(d_img, zf, k, alg_bytes, launches=20):
                     scratch.fill_(i & 0xFF)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-                lfm.predict_device(d_img, sym, X, Y, zf, T, FAMILY, k, stream=st)
+                fn()
                 e1.record(st)
                 e1.synchronize()
                 if i >= 2:
                     ms.append(e0.elapsed_time(e1))
             med = float(np.median(ms))
-            out[mode] = {"kernel_ms_median": round(med, 4), "kernel_ms_min": round(float(min(ms)), 4),
+            res[mode] = {"kernel_ms_median": round(med, 4), "kernel_ms_min": round(float(min(ms)), 4),
                          "frac": round(alg_bytes / (med / 1e3) / 1e9 / PEAK_HBM_GBS, 4)}
+        return res
+
+    with torch.cuda.stream(st):
+        out.update(timed(lambda: lfm.predict_device(d_img, sym, X, Y, zf, T, FAMILY, k, stream=st)))
+        out["copies"] = {"hipMemcpy_d2d": timed(lambda: sym.copy_(d_img)),
+                         "torch_add": timed(lambda: torch.add(d_img, 1, out=sym))}
     st.synchronize()
+    for mode in ("warm", "flushed"):
+        best = max(c[mode]["frac"] for c in out["copies"].values())
+        out[mode]["vs_best_copy"] = round(out[mode]["frac"] / best, 4) if best > 0 else None
     del scratch, sym
     torch.cuda.empty_cache()
     return out

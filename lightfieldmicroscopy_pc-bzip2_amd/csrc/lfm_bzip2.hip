@@ -2580,7 +2580,9 @@ struct HeapQuad {
     Ent e[4];
 };
 
-constexpr int kHeapQuads = (kMaxAlpha + 2 + 3) / 4;  // entries 0 .. 259
+// entries 0 .. 259, then one quad of sentinels (the grandchildren of every
+// node past 64 read as sentinels)
+constexpr int kHeapQuads = (kMaxAlpha + 2 + 3) / 4 + 1;
 
 // kL heaps with Ent entries in the LDS area hb (kHeapQuads * kL quads);
 // this lane's heap is (stream s, table tb)
@@ -2604,14 +2606,20 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
         };
         // rows are 8-byte aligned (258 words): pairs of words, a few loads ahead
         auto ld2 = [](const void* p, int i) { return *(const uint2*)((const uint32_t*)p + (i > 0 ? i : 0)); };
-        // a < b on weights (bits 10 and up) <=> a < (b with its node bits cleared)
+        // a < b on weights (bits 10 and up) <=> a < (b with its node bits
+        // cleared) <=> (a with its node bits set) < b
         constexpr Ent kW = ~(Ent)1023;
+        // every position past the heap holds kSent (greater than any entry:
+        // heights stop at 30), so the sift needs no bounds: a pop writes kSent
+        // where the last entry was, a push overwrites the first one
+        constexpr Ent kSent = ~(Ent)0;
         // downheap from the root with key k; returns the new root.  Per level:
         // the grandchildren quad is read first (it holds the children of
         // either next node), then the level is decided from the children in
         // registers; ea = address of the entry the key may land in, ca = the
         // children pair of zz (ea of the next level is ca + 4 * right)
-        auto sift = [&](int nHeap, Ent k) {
+        auto sift = [&](Ent k) {
+            const Ent kk = k | (Ent)1023;
             uint32_t zz = 1, ea = lb + ES, ca = lb + 2u * ES;
             Ent cx = ent(2), cy = ent(3), root = k;
             bool go = true, first = true;
@@ -2619,19 +2627,20 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
                 const uint32_t ga = min(zz, (uint32_t)kQuads - 1u) * QS + lb;
                 const HeapQuad<Ent> g = *(const HeapQuad<Ent>*)(hb + ga);
                 __builtin_amdgcn_sched_barrier(0);  // the read goes out before the level's compares
-                const uint32_t yy = zz << 1;
-                const bool r = yy < (uint32_t)nHeap && cy < (cx & kW);
+                const uint32_t r = (cy | (Ent)1023) < cx ? 1u : 0u;
                 const Ent ky = r ? cy : cx;
-                go = go && yy <= (uint32_t)nHeap && !(k < (ky & kW));
+                go = go && !(kk < ky);
                 *(Ent*)(hb + ea) = ky;  // a stopped lane's stray write is overwritten below
                 if (first) root = go ? ky : k;
                 first = false;
-                ea = go ? ca + (r ? ES : 0u) : ea;
-                ca = ga + (r ? 2u * ES : 0u);
-                zz = go ? yy + (r ? 1u : 0u) : zz;
+                const uint32_t zn = (zz << 1) | r, en = ca + r * ES;
+                ca = ga + r * (2u * ES);
+                ea = go ? en : ea;
+                zz = go ? zn : zz;
+                __builtin_amdgcn_sched_barrier(0);  // the quad is waited for last
                 cx = r ? g.e[2] : g.e[0];
                 cy = r ? g.e[3] : g.e[1];
-                if (!__any(go)) break;
+                if (!__builtin_amdgcn_ballot_w64(go)) break;
             }
             *(Ent*)(hb + ea) = k;
             return root;
@@ -2647,27 +2656,27 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             }
             return z;
         };
-        // upheap for the initial inserts (each climbs about log2(i) levels):
-        // every ancestor read first (one LDS latency), then the moves decided
-        // from registers; returns the final position
-        auto upheap_init = [&](uint32_t z, Ent k) {
-            constexpr int D = 10;  // z < 1024: nine levels to the root, then the sentinel entry 0
-            Ent anc[D];
+        // upheap for the initial inserts (z = i is the same in every lane
+        // still inserting): the positions z >> j on the way to the root are
+        // read at once, then every one is rewritten without a branch -- the
+        // parent's entry where the key climbs past it (lt), the key where it
+        // stops, the old entry above (the ancestors' weights only grow
+        // downwards, so lt holds for a prefix of the levels; position 0, the
+        // sentinel 0, ends it)
+        auto upheap_init = [&](uint32_t z) {
+            constexpr int D = 9;  // z < 512: z >> 9 is position 0
+            Ent v[D + 1];
 #pragma unroll
-            for (int j = 0; j < D; ++j) anc[j] = ent(z >> (j + 1));
-            bool go = true;
-            uint32_t zf = z;
+            for (int j = 0; j <= D; ++j) v[j] = ent(z >> j);  // v[0]: the key, the leaf at z
+            __builtin_amdgcn_sched_barrier(0);  // every read goes out before the first wait
+            const Ent k = v[0], kk = k | (Ent)1023;
+            bool below = true;  // the key climbed past the level below
 #pragma unroll
             for (int j = 0; j < D; ++j) {
-                go = go && k < (anc[j] & kW);  // the sentinel 0 stops it
-                if (go) {
-                    ent(z >> j) = anc[j];
-                    zf = z >> (j + 1);
-                }
-                if (!__any(go)) break;
+                const bool lt = kk < v[j + 1];
+                ent(z >> j) = lt ? v[j + 1] : (below || j == 0 ? k : v[j]);
+                below = lt;
             }
-            ent(zf) = k;
-            return zf;
         };
 #if LFM_HEAP_PROF
         unsigned long long hp_t0 = clock64(), hp_load = 0, hp_up = 0, hp_merge = 0, hp_t = 0;
@@ -2678,8 +2687,14 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             hp_t = clock64();
 #endif
             // leaves at heap positions 1 .. A first (an insertion's upheap only
-            // touches positions below it), then inserted in order
+            // touches positions below it), then inserted in order; sentinels
+            // past them
             ent(0) = 0;
+            for (int q = (A + 1) >> 2; q < kQuads; ++q) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (4 * q + j > A) ent((uint32_t)(4 * q + j)) = kSent;
+            }
             // 32 frequencies per batch of 16 loads (one memory latency per
             // batch, not per load: the compiler drains vmcnt at loop edges)
             for (int i0 = 1; i0 <= A; i0 += 32) {
@@ -2701,7 +2716,7 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
 #if LFM_HEAP_PROF
             { const unsigned long long t_ = clock64(); hp_load += t_ - hp_t; hp_t = t_; }
 #endif
-            for (int i = 1; i <= A; ++i) upheap_init((uint32_t)i, ent(i));
+            for (int i = 1; i <= A; ++i) upheap_init((uint32_t)i);
 #if LFM_HEAP_PROF
             { const unsigned long long t_ = clock64(); hp_up += t_ - hp_t; hp_t = t_; }
 #endif
@@ -2711,15 +2726,19 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             Ent top = ent(1);
             while (nHeap > 1) {
                 const Ent k1 = top;
-                const Ent k2 = sift(nHeap - 1, ent(nHeap));
+                const Ent l1 = ent(nHeap);
+                ent(nHeap) = kSent;
                 --nHeap;
-                const Ent r2 = sift(nHeap - 1, ent(nHeap));
+                const Ent k2 = sift(l1);
+                const Ent l2 = ent(nHeap);
+                ent(nHeap) = kSent;
                 --nHeap;
+                const Ent r2 = sift(l2);
                 ++nNodes;
                 parent[(uint32_t)k1 & 1023u] = (uint16_t)nNodes;
                 parent[(uint32_t)k2 & 1023u] = (uint16_t)nNodes;
                 const uint32_t h1 = (uint32_t)(k1 >> 10) & 31u, h2 = (uint32_t)(k2 >> 10) & 31u;
-                const uint32_t h = min(31u, 1u + max(h1, h2));
+                const uint32_t h = min(30u, 1u + max(h1, h2));
                 tooLong |= h > 17u ? 1u : 0u;
                 const Ent kn = ((((k1 >> 15) + (k2 >> 15)) << 5 | (Ent)h) << 10) | (Ent)nNodes;
                 ++nHeap;
@@ -2742,13 +2761,24 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             uint2 pw[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) pw[q] = ld2(parent, min(kc / 2 + 2 * q, (2 * kMaxAlpha) / 2 - 2));
+            // four nodes b .. b + 3 per LDS round trip: their parents' depths
+            // are read together, a parent inside the four (the root included)
+            // is taken from registers instead
 #pragma unroll
             for (int q = 15; q >= 0; --q) {
+                const int b = kc + 4 * q;
                 const uint32_t p4[4] = {pw[q].x & 0xFFFFu, pw[q].x >> 16, pw[q].y & 0xFFFFu, pw[q].y >> 16};
+                uint32_t d[4], dn[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) d[r] = dep(min(p4[r], 2u * kMaxAlpha));
 #pragma unroll
                 for (int r = 3; r >= 0; --r) {
-                    const int k = kc + 4 * q + r;
-                    if (k >= 1 && k < nNodes) dep(k) = (uint16_t)(dep(p4[r]) + 1u);
+                    const int k = b + r;
+                    uint32_t x = d[r];
+#pragma unroll
+                    for (int u = r + 1; u < 4; ++u) x = p4[r] == (uint32_t)(b + u) ? dn[u] : x;
+                    dn[r] = k == nNodes ? 0u : x + 1u;
+                    if (k >= 1 && k < nNodes) dep(k) = (uint16_t)dn[r];
                 }
             }
         }
