@@ -2150,14 +2150,14 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
         // first-occurrence lanes' one-hot ranks (8 words, DPP scans); a
         // serial loop over them (~27 per window, a readlane each) was
         // scalar-unit bound
+        // only the words from the lowest to the highest first-occurrence
+        // rank carry bits that count (usually one or two of the eight)
+        const bool isF = valid && !has_prev;
+        const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane(
+            (int)(wave_or_scan_excl32(isF ? 1u << (P0 >> 5) : 0u) | (isF ? 1u << (P0 >> 5) : 0u)), 63);
+        const uint32_t wlo = wm ? (uint32_t)__builtin_ctz(wm) : 8u, whi = wm ? 31u - (uint32_t)__clz(wm) : 0u;
         {
-            // only the words from the lowest to the highest first-occurrence
-            // rank carry bits that count (usually one or two of the eight)
-            const bool isF = valid && !has_prev;
             const uint32_t pw = P0 >> 5, pb = P0 & 31u;
-            const uint32_t wbit = isF ? 1u << pw : 0u;
-            const uint32_t wm = (uint32_t)__builtin_amdgcn_readlane((int)(wave_or_scan_excl32(wbit) | wbit), 63);
-            const uint32_t wlo = wm ? (uint32_t)__builtin_ctz(wm) : 8u, whi = wm ? 31u - (uint32_t)__clz(wm) : 0u;
             uint32_t cnt = 0;
             for (uint32_t wd = wlo; wd <= whi; ++wd) {
                 const uint32_t oh = (isF && pw == wd) ? (1u << pb) : 0u;
@@ -2168,32 +2168,41 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
             if (isF) m += cnt;
         }
         if (valid) mraw[j] = (uint8_t)m;
-        // list update: window symbols by last occurrence, then the rest
+        // list update: window symbols by last occurrence, then the rest.  The
+        // window symbols' old places (their first occurrences' P0) are below
+        // 32 * (whi + 1), and every entry past them keeps its place (nw
+        // removed before it, nw inserted in front), so only the blocks of 64
+        // places up to there move (place p = 64 q + lane)
         const bool is_last = valid && (M & gt) == 0ull;
         const uint64_t Lw = ballot64(is_last);
         const uint32_t nw = (uint32_t)__popcll(Lw);
+        const uint32_t nblk = whi / 2u + 1u;  // wave-uniform
         if (is_last) inw[wave][c] = 1;
         wsync();
         uint32_t sym[4], fl[4];
+        uint64_t fb[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t p = 4 * lane + q;
-            sym[q] = Lt[wave][p];
-            fl[q] = p < nin ? inw[wave][sym[q]] : 1u;
-        }
-        uint32_t rem_before = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rem_before += (uint32_t)__popcll(ballot64(fl[q] != 0) & lt);
-        wsync();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t p = 4 * lane + q;
-            if (!fl[q]) {
-                const uint32_t np = nw + p - rem_before;
-                Lt[wave][np] = (uint8_t)sym[q];
-                Pt[wave][sym[q]] = (uint8_t)np;
+        for (uint32_t q = 0; q < 4; ++q) {
+            if (q < nblk) {
+                const uint32_t p = 64u * q + lane;
+                sym[q] = Lt[wave][p];
+                fl[q] = p < nin ? inw[wave][sym[q]] : 1u;
+                fb[q] = ballot64(fl[q] != 0);
             }
-            rem_before += fl[q];
+        }
+        wsync();
+        uint32_t fl_blocks = 0;  // flagged places in the blocks before q
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            if (q < nblk) {
+                const uint32_t p = 64u * q + lane;
+                if (!fl[q]) {
+                    const uint32_t np = nw + p - (fl_blocks + (uint32_t)__popcll(fb[q] & lt));
+                    Lt[wave][np] = (uint8_t)sym[q];
+                    Pt[wave][sym[q]] = (uint8_t)np;
+                }
+                fl_blocks += (uint32_t)__popcll(fb[q]);
+            }
         }
         if (is_last) {
             const uint32_t np = (uint32_t)__popcll(Lw & gt);
