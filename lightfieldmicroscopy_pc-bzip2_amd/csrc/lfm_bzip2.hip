@@ -2177,7 +2177,7 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
         const uint64_t Lw = ballot64(is_last);
         const uint32_t nw = (uint32_t)__popcll(Lw);
         const uint32_t nblk = whi / 2u + 1u;  // wave-uniform
-        if (is_last) inw[wave][c] = 1;
+        if (isF) inw[wave][P0] = 1;  // flags by old place: the update reads them in order
         wsync();
         uint32_t sym[4], fl[4];
         uint64_t fb[4];
@@ -2186,7 +2186,7 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
             if (q < nblk) {
                 const uint32_t p = 64u * q + lane;
                 sym[q] = Lt[wave][p];
-                fl[q] = p < nin ? inw[wave][sym[q]] : 1u;
+                fl[q] = p < nin ? inw[wave][p] : 1u;
                 fb[q] = ballot64(fl[q] != 0);
             }
         }
@@ -2208,8 +2208,8 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
             const uint32_t np = (uint32_t)__popcll(Lw & gt);
             Lt[wave][np] = (uint8_t)c;
             Pt[wave][c] = (uint8_t)np;
-            inw[wave][c] = 0;
         }
+        if (isF) inw[wave][P0] = 0;
         wsync();
     }
 }
