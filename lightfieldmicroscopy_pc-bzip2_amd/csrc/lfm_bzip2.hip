@@ -2514,6 +2514,9 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
         lpack[v] = lp;
     }
     __syncthreads();
+    uint64_t lp_hot[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) lp_hot[f] = lpack[f];
     for (uint32_t g = t; g < nSel; g += kHuffThreads) {
         const uint32_t gs = g * kGSize, cnt = min(nMTF - gs, (uint32_t)kGSize);
         uint32_t w[kGSize / 2];
@@ -2529,10 +2532,21 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
                 w[q] = lo | (hi << 16);
             }
         }
-        // a group's cost under every table at once (10-bit fields, as huff_select)
+        // a group's cost under every table at once (10-bit fields, as
+        // huff_select); symbols 0 .. 3 (most of them) are counted in 8-bit
+        // fields and priced from registers, their lanes read the pad entry
+        // (one broadcast address instead of bank conflicts on 4 hot words)
+        uint32_t hot = 0;
         uint64_t acc = 0;
 #pragma unroll
-        for (int q = 0; q < kGSize / 2; ++q) acc += lpack[w[q] & 0xFFFFu] + lpack[w[q] >> 16];
+        for (int q = 0; q < kGSize / 2; ++q) {
+            const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
+            hot += lo < 4u ? 1u << (8u * lo) : 0u;
+            hot += hi < 4u ? 1u << (8u * hi) : 0u;
+            acc += lpack[lo < 4u ? (uint32_t)kMaxAlpha : lo] + lpack[hi < 4u ? (uint32_t)kMaxAlpha : hi];
+        }
+#pragma unroll
+        for (uint32_t f = 0; f < 4; ++f) acc += (uint64_t)((hot >> (8u * f)) & 0xFFu) * lp_hot[f];
         int bt = -1;
         uint32_t bc = 999999999u;
         for (int q = 0; q < nGroups; ++q) {
@@ -2541,15 +2555,12 @@ __global__ __launch_bounds__(kHuffThreads) void huff_select_reg(Batch B)
         }
         sel[g] = (uint8_t)bt;
         // symbols 0 .. 3 (RUNA, RUNB and the two smallest values: most of
-        // them) counted in 8-bit fields, the others by LDS atomics (the hot
-        // bins' atomics serialised on bank conflicts); a lane's other symbols
-        // land in its own junk word
-        uint32_t hot = 0;
+        // them) go to rfreq from their 8-bit fields, the others by LDS atomics
+        // (the hot bins' atomics serialised on bank conflicts); a lane's other
+        // symbols land in its own junk word
 #pragma unroll
         for (int q = 0; q < kGSize / 2; ++q) {
             const uint32_t lo = w[q] & 0xFFFFu, hi = w[q] >> 16;
-            hot += lo < 4u ? 1u << (8u * lo) : 0u;
-            hot += hi < 4u ? 1u << (8u * hi) : 0u;
             atomicAdd(lo >= 4u && lo != (uint32_t)kMaxAlpha ? &rfreq[bt][lo] : &junk[t], 1u);
             atomicAdd(hi >= 4u && hi != (uint32_t)kMaxAlpha ? &rfreq[bt][hi] : &junk[t], 1u);
         }
