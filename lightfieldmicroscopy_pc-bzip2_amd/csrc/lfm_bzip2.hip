@@ -747,6 +747,10 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
         if (t < 256) cnt_u[t] = cnt_s[t] = 0;
         if (t == 0) undecided = n_unsorted = 0;
         __syncthreads();
+        // unsorted rotations starting with byte 0 (the high bytes of small
+        // 16-bit symbols: about half of all rotations) are counted in a
+        // register -- their LDS atomics all hit one word and serialise
+        uint32_t u_zero = 0;
         BktPart nx = bucket_fetch(T, n, 0);
         for (uint32_t i0 = 0, it = 0; i0 < n; i0 += kBktTile, ++it) {
             const BktPart cur = nx;
@@ -760,9 +764,11 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
                 if (ty == 2u) undecided = 1u;
                 else if (mode == kModeFull || ty == (mode == kModeSortB ? 1u : 0u))
                     atomicAdd(&hist[bkt_slot<BITS>((a << (BITS - 8)) | (b >> (16 - BITS)))], 1u);
+                else if (a == 0u) ++u_zero;
                 else atomicAdd(&cnt_u[a], 1u);
             }
         }
+        if (u_zero) atomicAdd(&cnt_u[0], u_zero);
         __syncthreads();
         if (mode == kModeFull) break;
         if (undecided) {
