@@ -751,6 +751,10 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
         // 16-bit symbols: about half of all rotations) are counted in a
         // register -- their LDS atomics all hit one word and serialise
         uint32_t u_zero = 0;
+        // sorted rotations in buckets a << (BITS - 8) for a < 4 (a small low
+        // byte, then a zero high byte: the hottest buckets) likewise, in
+        // 16-bit register fields
+        uint32_t hot01 = 0, hot23 = 0;
         BktPart nx = bucket_fetch(T, n, 0);
         for (uint32_t i0 = 0, it = 0; i0 < n; i0 += kBktTile, ++it) {
             const BktPart cur = nx;
@@ -762,13 +766,26 @@ __global__ __launch_bounds__(kBucketThreads) __attribute__((amdgpu_waves_per_eu(
                 const uint32_t a = tile[kTOff + k], b = tile[kTOff + 1 + k];
                 const uint32_t ty = mode == kModeFull ? 3u : rot_type(tile, k, a, b);
                 if (ty == 2u) undecided = 1u;
-                else if (mode == kModeFull || ty == (mode == kModeSortB ? 1u : 0u))
-                    atomicAdd(&hist[bkt_slot<BITS>((a << (BITS - 8)) | (b >> (16 - BITS)))], 1u);
+                else if (mode == kModeFull || ty == (mode == kModeSortB ? 1u : 0u)) {
+                    const uint32_t key = (a << (BITS - 8)) | (b >> (16 - BITS));
+                    if (key < (4u << (BITS - 8)) && (key & ((1u << (BITS - 8)) - 1u)) == 0u) {
+                        const uint32_t inc = 1u << (16u * (a & 1u));
+                        if (a < 2u) hot01 += inc;
+                        else hot23 += inc;
+                    } else {
+                        atomicAdd(&hist[bkt_slot<BITS>(key)], 1u);
+                    }
+                }
                 else if (a == 0u) ++u_zero;
                 else atomicAdd(&cnt_u[a], 1u);
             }
         }
         if (u_zero) atomicAdd(&cnt_u[0], u_zero);
+#pragma unroll
+        for (uint32_t h = 0; h < 4; ++h) {
+            const uint32_t c = ((h < 2u ? hot01 : hot23) >> (16u * (h & 1u))) & 0xFFFFu;
+            if (c) atomicAdd(&hist[bkt_slot<BITS>(h << (BITS - 8))], c);
+        }
         __syncthreads();
         if (mode == kModeFull) break;
         if (undecided) {
