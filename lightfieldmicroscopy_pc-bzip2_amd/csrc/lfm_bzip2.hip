@@ -53,12 +53,6 @@
 #include <vector>
 #include "lfm_hip.h"
 
-#ifndef LFM_HEAP_PROF
-#define LFM_HEAP_PROF 0  // huff_lengths_heap phase clocks by printf (timing variants only)
-#endif
-#ifndef LFM_IND_PROF
-#define LFM_IND_PROF 0  // bwt_induce phase clocks by printf (timing variants only; 0 in the library)
-#endif
 
 namespace lfm {
 namespace bz {
@@ -1762,25 +1756,14 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
     __syncthreads();
     issue(0);
     stage(0);
-#if LFM_IND_PROF
-    unsigned long long pt0 = 0, pt_issue = 0, pt_steps = 0, pt_stage = 0, pt_flush = 0, pt_total = clock64();
-    uint32_t c_steps = 0, c_rounds = 0, c_dist = 0, c_text = 0, c_far = 0, c_ind = 0;
-#define IND_T(x) do { const unsigned long long t_ = clock64(); x += t_ - pt0; pt0 = t_; } while (0)
-#else
-#define IND_T(x) do { } while (0)
-#endif
     bool bad = false;  // inconsistent counts or a pending entry no earlier lane places (never)
     uint32_t org = ~0u;
     for (uint32_t v0 = 0; v0 < n && !bad; v0 += kIndBlock) {
-#if LFM_IND_PROF
-        pt0 = clock64();
-#endif
         // the next block's ring slots held the previous block: not placed yet
 #pragma unroll
         for (uint32_t k = 0; k < kIndSlices; ++k) ring[(v0 + kIndBlock + 64 * k + lane) % kIndRing].x = kIndPend;
         const bool more = v0 + kIndBlock < n;
         if (more) issue(v0 + kIndBlock);
-        IND_T(pt_issue);
         // steps of kIndStepSlices slices: item k of lane l is position
         // vs + 64 k + l, and the scan order is (k, l)
         for (uint32_t vs = v0; vs < min(n, v0 + kIndBlock) && !bad; vs += 64 * kIndStepSlices) {
@@ -1793,15 +1776,9 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                 todo[k] = __ballot(v < n);
                 e[k] = ring[v % kIndRing];
             }
-#if LFM_IND_PROF
-            ++c_steps;
-#endif
             // rounds up to the first pending entry: one round unless an entry
             // of the step is placed by an earlier one of the same step
             for (;;) {
-#if LFM_IND_PROF
-                ++c_rounds;
-#endif
                 uint64_t act[KS], pend[KS], anyp = 0;
 #pragma unroll
                 for (int k = 0; k < KS; ++k) {
@@ -1852,9 +1829,6 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                         tot_of[k] = 0;
                     }
                     while (left) {
-#if LFM_IND_PROF
-                        ++c_dist;
-#endif
                         uint32_t bl = 0;
                         bool got = false;
 #pragma unroll
@@ -1912,18 +1886,11 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                             const uint32_t x = text_prev4(T, n, p + 1);  // T[p-1] .. T[p-4]
                             plo[k] = p | (3u << 20) | kIndPlaced | ((x & 0xFFu) << 24);
                             phi[k] = ((x >> 8) & 0xFFFFFFu) | (lo & 0xFF000000u);
-#if LFM_IND_PROF
-                            ++c_text;
-#endif
                         }
                     }
 #pragma unroll
                     for (int k = 0; k < KS; ++k) {
                         const bool near = dest[k] < v0 + kIndRing;
-#if LFM_IND_PROF
-                        c_ind += ind[k];
-                        c_far += ind[k] && !near;
-#endif
                         if (ind[k] && near) ring[dest[k] % kIndRing] = make_uint2(plo[k], phi[k]);
                         if (ind[k] && !near) E[qof(dest[k])] = make_uint2(plo[k], phi[k]);
                     }
@@ -1940,19 +1907,9 @@ __global__ __launch_bounds__(64) void bwt_induce(Batch B)
                 for (int k = 0; k < KS; ++k) e[k] = ring[(vs + 64 * k + lane) % kIndRing];
             }
         }
-        IND_T(pt_steps);
         if (!bad) flush(v0);
-        IND_T(pt_flush);
         if (more && !bad) stage(v0 + kIndBlock);
-        IND_T(pt_stage);
     }
-#if LFM_IND_PROF
-    if (lane == 0 && s < 4)
-        printf("induce prof s %u n %u mode %u: total %llu issue %llu steps %llu flush %llu stage %llu | steps %u "
-               "rounds %u distinct %u induced(lane0) %u text %u far %u\n", s, n, mode, clock64() - pt_total,
-               pt_issue, pt_steps, pt_flush, pt_stage, c_steps, c_rounds, c_dist, c_ind, c_text, c_far);
-#endif
-#undef IND_T
     if (bad && lane == 0) B.flags[s] |= kFlagHost;  // the host library redoes the stream
     if (org != ~0u) B.orig_ptr[s] = org;
 }
@@ -2721,14 +2678,8 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
                 below = lt;
             }
         };
-#if LFM_HEAP_PROF
-        unsigned long long hp_t0 = clock64(), hp_load = 0, hp_up = 0, hp_merge = 0, hp_t = 0;
-#endif
         int retries = 0, nNodes = A;
         while (true) {
-#if LFM_HEAP_PROF
-            hp_t = clock64();
-#endif
             // leaves at heap positions 1 .. A first (an insertion's upheap only
             // touches positions below it), then inserted in order; sentinels
             // past them
@@ -2756,13 +2707,7 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
                     if (i + 1 <= A) ent(i + 1) = ((Ent)w1 << 15) | (Ent)(i + 1);
                 }
             }
-#if LFM_HEAP_PROF
-            { const unsigned long long t_ = clock64(); hp_load += t_ - hp_t; hp_t = t_; }
-#endif
             for (int i = 1; i <= A; ++i) upheap_init((uint32_t)i);
-#if LFM_HEAP_PROF
-            { const unsigned long long t_ = clock64(); hp_up += t_ - hp_t; hp_t = t_; }
-#endif
             int nHeap = A;
             nNodes = A;
             uint32_t tooLong = 0;
@@ -2787,15 +2732,9 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
                 ++nHeap;
                 top = upheap((uint32_t)nHeap, kn) == 1u ? kn : r2;
             }
-#if LFM_HEAP_PROF
-            { const unsigned long long t_ = clock64(); hp_merge += t_ - hp_t; hp_t = t_; }
-#endif
             if (!tooLong) break;
             ++retries;
         }
-#if LFM_HEAP_PROF
-        const unsigned long long hp_t1 = clock64();
-#endif
         if (retries) atomicAdd(B.wide_cnt + 1, (uint32_t)retries);  // statistics (LFM_BZ2_STATS)
         // depths top-down (a parent is created after its children)
         dep(nNodes) = 0;
@@ -2826,11 +2765,6 @@ __device__ __forceinline__ void heap_code_lengths(const Batch& B, char* hb, uint
             }
         }
         for (int i = 1; i <= A; ++i) len[i - 1] = (uint8_t)dep(i);
-#if LFM_HEAP_PROF
-        if (lane == 0 && s < 3 && tb == 0)
-            printf("heap prof s %u A %d retries %d: total %llu load %llu upinit %llu merge %llu depth %llu\n", s, A,
-                   retries, clock64() - hp_t0, hp_load, hp_up, hp_merge, clock64() - hp_t1);
-#endif
     }
 }
 
