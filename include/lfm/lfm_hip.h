@@ -49,6 +49,18 @@ int lfm_hip_predict(const uint16_t* d_in, const uint16_t* d_prev, uint16_t* d_ou
  * angle / space families (their residual is not invertible). */
 int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H, int nframes,
                       int T, int family, int predictor, int video_bit, int z0, void* stream);
+/* lfm_hip_unpredict without the synchronisation: the kernels are queued on
+ * `stream` and the launch's status word is copied into *h_status (pinned host
+ * memory) behind them; once the stream has passed that point the caller hands
+ * it to lfm_hip_unpredict_check.  The pipelined decode (gpu_decode) checks
+ * each chunk's words at the event its download already waits for. */
+int lfm_hip_unpredict_async(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
+                            int nframes, int T, int family, int predictor, int video_bit, int z0, int* h_status,
+                            void* stream);
+/* LFM_HIP_OK when a status word says the pixels are valid (0, or a band
+ * hand-over timeout repaired on the device, reported on stderr), else
+ * LFM_HIP_ERUNTIME. */
+int lfm_hip_unpredict_check(int status);
 
 /* The seven spatial candidates of one frame (predictors 1..7, symbolized) in
  * one launch: candidate k goes to d_out7 + (k-1)*W*H. */

@@ -2029,6 +2029,8 @@ struct DecodeBuffers {
     size_t cap[N] = {};
     uint32_t* hs[kSlots] = {};  // pinned: lens then flags, per slot
     size_t hs_cap[kSlots] = {};
+    int* us = nullptr;          // pinned: the inverse predictor's status words, per (chunk, volume piece)
+    size_t us_cap = 0;
     Staging down;                            // the download thread's pinned chunks
     DecodeBuffers() = default;
     DecodeBuffers(const DecodeBuffers&) = delete;
@@ -2041,6 +2043,9 @@ struct DecodeBuffers {
             p[i] = nullptr;
             cap[i] = 0;
         }
+        if (us) (void)hipHostFree(us);
+        us = nullptr;
+        us_cap = 0;
         for (int k = 0; k < kSlots; ++k) {
             if (hs[k]) (void)hipHostFree(hs[k]);
             hs[k] = nullptr;
@@ -2092,6 +2097,19 @@ struct DecodeBuffers {
         }
         hs_cap[k] = count;
         return hs[k];
+    }
+    int* ustatus(size_t count)
+    {
+        if (us_cap >= count) return us;
+        if (us) (void)hipHostFree(us);
+        us = nullptr;
+        us_cap = 0;
+        if (hipHostMalloc((void**)&us, count * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+            us = nullptr;
+            return nullptr;
+        }
+        us_cap = count;
+        return us;
     }
 };
 
@@ -2169,6 +2187,10 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     void *d_pay = nullptr, *d_sym = nullptr, *d_out = nullptr, *d_ws[DecodeBuffers::kSlots] = {},
          *d_blk[DecodeBuffers::kSlots] = {};
     uint32_t* hs[DecodeBuffers::kSlots] = {};
+    // inverse predictor status words: chunk c's volume pieces at us[c * (spc + 1) ..]
+    // (a chunk's slabs lie in at most spc volumes)
+    int* us = nullptr;
+    const uint64_t us_per = spc + 1;
     if (DB.begin()) {
         d_pay = DB.get(DecodeBuffers::PAY, offs[nb] + 64);
         d_sym = DB.get(DecodeBuffers::SYM, img_bytes);
@@ -2178,8 +2200,12 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             d_blk[q] = DB.get(DecodeBuffers::BLK0 + q, batch * block_bytes);
             hs[q] = DB.status(q, batch);
         }
+        if (predicted) {
+            us = DB.ustatus(nch * us_per);
+            if (us) std::fill(us, us + nch * us_per, 0);
+        }
     }
-    bool have = DB.st[0] && d_pay && d_sym && (!predicted || d_out);
+    bool have = DB.st[0] && d_pay && d_sym && (!predicted || (d_out && us));
     for (int q = 0; q < nslot; ++q) have = have && d_ws[q] && d_blk[q] && hs[q];
     if (!have) {
         DB.release();
@@ -2261,11 +2287,15 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             // a temporal first frame (video, odd z) reads the previous chunk's
             // last decoded frame: wait for that chunk's inverse predictor
             if (video && c > 0 && hipStreamWaitEvent(st, cev[c - 1], 0) != hipSuccess) return 3;
-            for (uint64_t f = f0; f < f1;) {  // per volume
+            uint64_t piece = 0;
+            for (uint64_t f = f0; f < f1; ++piece) {  // per volume
                 const uint64_t v = f / Z, z0 = f % Z, n = std::min<uint64_t>(f1, (v + 1) * Z) - f;
                 const uint16_t* prev = z0 > 0 ? (const uint16_t*)d_out + (f - 1) * W * H : nullptr;
-                const int hr = lfm_hip_unpredict((const uint16_t*)d_sym + f * W * H, prev, (uint16_t*)d_out + f * W * H,
-                                                 (int)W, (int)H, (int)n, h.Nnum, family, k, video, (int)z0, st);
+                if (piece >= us_per) return 3;  // (cannot happen: see us_per)
+                // queued only: its status word is checked with the download
+                const int hr = lfm_hip_unpredict_async((const uint16_t*)d_sym + f * W * H, prev,
+                                                       (uint16_t*)d_out + f * W * H, (int)W, (int)H, (int)n, h.Nnum,
+                                                       family, k, video, (int)z0, us + c * us_per + piece, st);
                 if (hr == LFM_HIP_ENOTINV) {
                     std::printf("ERROR: frames of this file cannot be inverted (temporal angle/space predictor)\n");
                     return 3;
@@ -2302,8 +2332,20 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             const size_t o0 = f0 * frame_bytes, n = (f1 - f0) * frame_bytes;
             const uint8_t* src = (const uint8_t*)(predicted ? d_out : d_sym) + o0;
             hipStream_t st = DB.st[c % nslot];
-            if (hipEventSynchronize(cev[c]) != hipSuccess ||
-                (!sdma_staged_d2h(img + o0, src, n, threads, DB.down) &&
+            if (hipEventSynchronize(cev[c]) != hipSuccess) {
+                drc = 3;
+                return;
+            }
+            // the chunk's inverse predictor launches: a hand-over that timed
+            // out and was not repaired on the device fails the read
+            if (predicted)
+                for (uint64_t i = 0; i < us_per; ++i)
+                    if (lfm_hip_unpredict_check(us[c * us_per + i]) != LFM_HIP_OK) {
+                        std::printf("ERROR: the inverse predictor did not complete (band hand-over timed out)\n");
+                        drc = 3;
+                        return;
+                    }
+            if ((!sdma_staged_d2h(img + o0, src, n, threads, DB.down) &&
                  (!staged_d2h(img + o0, src, n, st, threads, DB.down) || hipStreamSynchronize(st) != hipSuccess))) {
                 drc = 3;
                 return;

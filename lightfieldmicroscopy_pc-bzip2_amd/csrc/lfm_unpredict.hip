@@ -20,6 +20,8 @@
 // odd temporal frames on their decoded predecessors).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <climits>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -71,14 +73,24 @@ struct UnFrames {
     uint16_t* out;         // nz decoded frames
     int W, H, T, nz, z0, video;
     int first, step;       // this launch decodes local frames first, first + step, ...
-    // band4 / band5 hand-over: a wait gives up after spin_limit polls (a
-    // band that never sees its producer must not hang the device) and then
-    // sets *err (band5: global memory, checked by the launcher, which re-runs
-    // the frames through band4); null = not reported
+    // band4 / band5 hand-over: a wait gives up after wait_ticks of the
+    // 100 MHz real-time clock (or spin_limit polls: tests force a timeout),
+    // ORs err_bit into *status (global memory) and from then on every wait of
+    // that band returns at once; a band5 wait also gives up as soon as any
+    // other band has set the bit.  The launch that follows a band5 launch
+    // (band4, `repair`) re-runs every frame when bit 1 is set.
     int spin_limit;
-    int* err;
+    unsigned err_bit;
+    unsigned* status;
+    uint64_t wait_ticks;
+    int repair;            // band4 only: run only if a band5 hand-over gave up
 };
-constexpr int kSpinLimit = 1 << 24;  // ~0.45 s of s_sleep 1 polls
+// status bits (the control block's word 0, reported to the caller)
+constexpr unsigned kStBand5 = 1u;   // a band5 hand-over timed out (frames re-run through band4)
+constexpr unsigned kStBand4 = 2u;   // a band4 hand-over timed out: the pixels are not valid
+// control block (hipMalloc'd, pooled): word 0 status, word 32 the band5
+// ticket counter, words 33.. the band progress words (0 before the launch)
+constexpr int kCtlTicket = 32, kCtlPos = 33;
 
 template <int FAM, int K>
 __global__ __launch_bounds__(64) void unpredict_band(UnFrames p)
@@ -444,20 +456,50 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
     const int W = p.W, H = p.H, T = p.T, TT = T + 1;
     const int nbands = (H + 63) / 64, kend = W + 63, stride = W + 64 + 3 * kSync;
     const int prodw = (wv + NW - 1) % NW;
-    // (bounded: a hand-over that times out sets *p.err -- the launcher then
-    // discards the band5 result and re-runs the frames -- never a hang)
+    // (bounded in time: a wait that gives up sets its bit in *p.status -- a
+    // band5 launch is then re-run through band4 on the device -- and the band
+    // runs on without waiting; never a hang.)  Progress is monotonic, so a
+    // stale read can only under-report it: it delays a band, never releases
+    // one early.
     // XCU: `seen` is the producer's progress as last read; a read is issued
     // after every wait and consumed at the next one (a round later, so it has
     // returned), and a wait that `seen` already satisfies costs no load
     int seen = -1, pending = -1;
-    const int spin_limit = p.spin_limit;
+    bool dead = false;  // this band gave up waiting: later waits return at once
     auto wait_ge = [&](int need) {
         if constexpr (XCU) seen = max(seen, __builtin_amdgcn_readfirstlane(pending));
-        for (int spin = 0; spin < spin_limit && seen < need; ++spin) {
-            seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope));
-            if (seen < need) __builtin_amdgcn_s_sleep(1);
+        if (seen < need && !dead) {
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            for (int spin = 1;; ++spin) {
+                seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope));
+                if (seen >= need) break;
+                if (spin >= p.spin_limit) {
+                    dead = true;
+                    break;
+                }
+                if ((spin & 63) == 0) {
+                    if constexpr (XCU) {
+                        // another band gave up: this launch is re-run anyway
+                        if (__builtin_amdgcn_readfirstlane(
+                                __hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & p.err_bit) {
+                            dead = true;
+                            break;
+                        }
+                        // a long wait also drops this CU's cached lines (an
+                        // agent acquire), so no cache level can keep serving
+                        // an old progress word
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    }
+                    if ((uint64_t)wall_clock64() - t0 > p.wait_ticks) {
+                        dead = true;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (dead && r == 0)
+                __hip_atomic_fetch_or(p.status, p.err_bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (seen < need && p.err && r == 0) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (XCU) pending = __hip_atomic_load(pos + prodw, __ATOMIC_RELAXED, kScope);
         // XCU: every later load of the band above's rows is an sc1 load
         // (hload), so this only keeps the compiler from hoisting them
@@ -645,6 +687,9 @@ __global__ __launch_bounds__(512) void unpredict_band4(UnFrames p, int NW)
     __shared__ int pos[8];  // progress of each wave (band * stride + steps done)
     const int fz = p.first + (int)blockIdx.x * p.step;
     if (fz >= p.nz) return;
+    // the re-run after a band5 launch: nothing to do unless one of its
+    // hand-overs gave up (that launch's bit is in the status word)
+    if (p.repair && !(__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStBand5)) return;
     const int wv = threadIdx.x >> 6, TT = p.T + 1;
     if (threadIdx.x < (unsigned)NW) pos[threadIdx.x] = -1;
     __syncthreads();
@@ -656,19 +701,30 @@ __global__ __launch_bounds__(512) void unpredict_band4(UnFrames p, int NW)
 }
 
 // band5: the band pipeline spread over the whole chip -- one single-wave
-// workgroup per (band, frame), blockIdx = band * nfr + frame, so every band is
-// dispatched after the band above it (the one it waits for) and, with nfr a
-// multiple of 8, all bands of a frame share an XCD (one L2).  Progress words
-// (one per band, -1 before the launch) live in global memory.  Config 3: 2048
-// waves over 256 CUs instead of 64 workgroups of 8 waves on 64 CUs.
+// workgroup per (band, frame).  HIP promises neither a dispatch order nor a
+// workgroup -> XCD placement, so a workgroup does not take its band from
+// blockIdx: its first act is to draw a ticket (an agent-scope atomic add on
+// the control block) and it decodes band ticket / nfr of frame ticket % nfr.
+// Tickets go out in the order the workgroups actually started, so the band a
+// workgroup waits for (ticket - nfr) belongs to a workgroup that is already
+// resident, and the chain of waits always ends at a running band 0, wherever
+// and whenever the workgroups were placed.  Progress words (one per band, 0
+// before the launch) live in the same hipMalloc'd control block: bands
+// publish with write-through (sc1) stores after draining their pixel stores
+// and poll with sc1 loads (MI355X_MICROARCH.md, visibility, write-through
+// form).  Config 3: 2048 waves over 256 CUs instead of 64 workgroups of 8
+// waves on 64 CUs.
 template <int FAM, int K>
-__global__ __launch_bounds__(64) void unpredict_band5(UnFrames p, int* pos_all, int nbands, int nfr)
+__global__ __launch_bounds__(64) void unpredict_band5(UnFrames p, int* ctl, int nbands, int nfr)
 {
     extern __shared__ __attribute__((aligned(16))) uint16_t lds5[];
-    const int b = (int)blockIdx.x / nfr, fi = (int)blockIdx.x - b * nfr;
+    int t = 0;
+    if (threadIdx.x == 0) t = __hip_atomic_fetch_add(ctl + kCtlTicket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __builtin_amdgcn_readfirstlane(t);
+    const int b = t / nfr, fi = t - b * nfr;
     const int fz = p.first + fi * p.step;
-    if (fz >= p.nz || b >= nbands) return;
-    int* pos = pos_all + (size_t)fi * nbands;
+    if (fz >= p.nz || b >= nbands) return;  // (the grid is exactly nbands * nfr)
+    int* pos = ctl + kCtlPos + (size_t)fi * nbands;
     if (p.video && ((p.z0 + fz) & 1)) band4<FAM, K, true, true>(p, fz, nbands, b, lds5, 0, 64 * kRing, pos);
     else band4<FAM, K, false, true>(p, fz, nbands, b, lds5, 0, 64 * kRing, pos);
 }
@@ -714,62 +770,148 @@ static int band4_waves(const UnFrames& p)
     return nw >= 2 ? nw : 0;
 }
 
-// hand-over poll limit: kSpinLimit, or LFM_UNPREDICT_SPIN (tests force a
-// timeout with a tiny limit); LFM_UNPREDICT_FALLBACK=0 reports a band5 timeout
-// as an error instead of re-running the frames through band4
-static int spin_limit()
+// Hand-over limits.  LFM_UNPREDICT_WAIT_MS (default 500): a band5 / band4 wait
+// gives up after that long on the device's 100 MHz real-time clock.
+// LFM_UNPREDICT_SPIN (tests): band5 waits give up after that many polls.
+// LFM_UNPREDICT_FALLBACK=0: a band5 timeout is reported as an error instead of
+// re-running the frames through band4.  Read per call (tests set them in the
+// process).
+static int band5_spin_limit()
 {
     const char* e = std::getenv("LFM_UNPREDICT_SPIN");
-    return e ? std::max(1, std::atoi(e)) : kSpinLimit;
+    return e ? std::max(1, std::atoi(e)) : INT_MAX;
+}
+
+static bool fallback_enabled()
+{
+    const char* f = std::getenv("LFM_UNPREDICT_FALLBACK");
+    return !(f && std::atoi(f) == 0);
+}
+
+static uint64_t wait_ticks()
+{
+    const char* e = std::getenv("LFM_UNPREDICT_WAIT_MS");
+    const long ms = e ? std::max(1l, std::atol(e)) : 500l;
+    int khz = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+        khz <= 0)
+        khz = 100000;  // the gfx9 real-time clock: 100 MHz
+    return (uint64_t)khz * (uint64_t)ms;
+}
+
+// Control blocks: device words (hipMalloc) for the status, the band5 ticket
+// and the progress words.  A block is handed to one call at a time and taken
+// again only once the event recorded behind that call's last use has fired,
+// so concurrent decodes on several streams never share progress words.  (A
+// stream-ordered pool allocation per launch -- hipMallocAsync / hipFreeAsync,
+// round 5 -- gave no such guarantee across streams and is not the memory
+// type whose cross-XCD behaviour MI355X_MICROARCH.md measured.)
+struct CtlBlock {
+    int dev = -1;
+    int* d = nullptr;
+    size_t words = 0;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+};
+
+static std::mutex& ctl_mu()
+{
+    static std::mutex m;
+    return m;
+}
+
+static std::vector<CtlBlock*>& ctl_pool()
+{
+    static std::vector<CtlBlock*> v;  // (process lifetime: a handful per device)
+    return v;
+}
+
+static CtlBlock* ctl_acquire(size_t words)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(ctl_mu());
+    CtlBlock* got = nullptr;
+    int mine = 0;
+    for (CtlBlock* c : ctl_pool()) {
+        if (c->dev != dev) continue;
+        ++mine;
+        if (!c->busy && c->words >= words && hipEventQuery(c->done) == hipSuccess) {
+            got = c;
+            break;
+        }
+    }
+    (void)hipGetLastError();  // (a pending event's hipErrorNotReady)
+    if (!got && mine >= 64) {  // bounded pool: wait for the first idle block of the size
+        for (CtlBlock* c : ctl_pool())
+            if (c->dev == dev && !c->busy && c->words >= words && hipEventSynchronize(c->done) == hipSuccess) {
+                got = c;
+                break;
+            }
+    }
+    if (!got) {
+        got = new CtlBlock;
+        got->dev = dev;
+        got->words = std::max<size_t>(words, 1 << 16);
+        if (hipMalloc((void**)&got->d, got->words * sizeof(int)) != hipSuccess ||
+            hipEventCreateWithFlags(&got->done, hipEventDisableTiming) != hipSuccess) {
+            if (got->d) (void)hipFree(got->d);
+            (void)hipGetLastError();
+            delete got;
+            return nullptr;
+        }
+        ctl_pool().push_back(got);
+    }
+    got->busy = true;
+    return got;
+}
+
+static void ctl_release(CtlBlock* c, hipStream_t st)
+{
+    std::lock_guard<std::mutex> lk(ctl_mu());
+    (void)hipEventRecord(c->done, st);
+    c->busy = false;
 }
 
 template <int FAM, int K_>
-static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool no_band5 = false)
+static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, int* ctl)
 {
-    if (band4_waves(p) && !no_band5) {
+    if (band4_waves(p)) {
         const int nbands = (p.H + 63) / 64;
         const size_t lds = (size_t)(64 * kRing + (p.T + 1) * kHand) * 2;
-        int* pos = nullptr;
-        const size_t pbytes = (size_t)grid * nbands * sizeof(int);
-        // progress words, then the timeout word
-        if (hipMallocAsync((void**)&pos, pbytes + sizeof(int), st) != hipSuccess) return hipErrorOutOfMemory;
-        hipError_t e = hipMemsetAsync(pos, 0xFF, pbytes, st);  // -1: no progress yet
-        if (e == hipSuccess) e = hipMemsetAsync(pos + (size_t)grid * nbands, 0, sizeof(int), st);
+        // ticket and progress words of this launch start at 0 (every wait
+        // needs a progress > 0); the status word accumulates over the call
+        hipError_t e = hipMemsetAsync(ctl + kCtlTicket, 0, (size_t)(1 + grid * nbands) * sizeof(int), st);
         UnFrames pt = p;
-        pt.spin_limit = spin_limit();
-        pt.err = pos + (size_t)grid * nbands;
+        pt.status = (unsigned*)ctl;
+        pt.err_bit = kStBand5;
+        pt.spin_limit = band5_spin_limit();
+        pt.repair = 0;
         if (e == hipSuccess) {
-            hipLaunchKernelGGL((unpredict_band5<FAM, K_>), dim3(grid * nbands), dim3(64), lds, st, pt, pos, nbands,
+            hipLaunchKernelGGL((unpredict_band5<FAM, K_>), dim3(grid * nbands), dim3(64), lds, st, pt, ctl, nbands,
                                grid);
             e = hipGetLastError();
         }
-        // a band that gave up waiting (its producer never got a CU, e.g. the
-        // chip shared with other work) decoded from rows that were not ready:
-        // the launch's result is discarded and every frame re-run through
-        // band4, whose bands share one workgroup and so are co-resident
-        int timed_out = 0;
-        if (e == hipSuccess) e = hipMemcpyAsync(&timed_out, pt.err, sizeof(int), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        (void)hipFreeAsync(pos, st);
-        if (e == hipSuccess && timed_out) {
-            static const bool fallback = [] {
-                const char* f = std::getenv("LFM_UNPREDICT_FALLBACK");
-                return !(f && std::atoi(f) == 0);
-            }();
-            std::fprintf(stderr, "lfm: inverse predictor band hand-over timed out (band5, %d x %d bands)%s\n", grid,
-                         nbands, fallback ? "; frames re-run through band4" : "");
-            if (!fallback) e = hipErrorLaunchTimeOut;
-            else e = launch_band2<FAM, K_>(p, grid, st, true);
+        // re-run on the device, no host round trip: a band that gave up
+        // decoded from rows that were not ready, so when the status word
+        // carries kStBand5 every frame of the launch runs again through band4
+        // (one workgroup per frame: its bands share one workgroup, so they are
+        // co-resident); otherwise its workgroups return at once
+        if (e == hipSuccess && fallback_enabled()) {
+            const int nw = band4_waves(p);
+            const size_t lds4 = (size_t)nw * (64 * kRing + (p.T + 1) * kHand) * 2;
+            const void* fn4 = (const void*)unpredict_band4<FAM, K_>;
+            if (hipFuncSetAttribute(fn4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4) != hipSuccess)
+                return hipErrorInvalidValue;
+            UnFrames pr = p;
+            pr.status = (unsigned*)ctl;
+            pr.err_bit = kStBand4;
+            pr.spin_limit = INT_MAX;
+            pr.repair = 1;
+            hipLaunchKernelGGL((unpredict_band4<FAM, K_>), dim3(grid), dim3(64 * nw), lds4, st, pr, nw);
+            e = hipGetLastError();
         }
         return e;
-    }
-    if (const int nw = band4_waves(p)) {
-        const size_t lds = (size_t)nw * (64 * kRing + (p.T + 1) * kHand) * 2;
-        const void* fn4 = (const void*)unpredict_band4<FAM, K_>;
-        if (hipFuncSetAttribute(fn4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return hipErrorInvalidValue;
-        hipLaunchKernelGGL((unpredict_band4<FAM, K_>), dim3(grid), dim3(64 * nw), lds, st, p, nw);
-        return hipGetLastError();
     }
     const size_t lds = band2_lds(p);
     // band3 reads a step's far neighbours one step early: T >= 2
@@ -783,13 +925,13 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, bool
 }
 
 template <int FAM>
-static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st)
+static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st, int* ctl)
 {
     const int grid = (p.nz - p.first + p.step - 1) / p.step;
     if (grid <= 0) return hipSuccess;
     if (band2_ok(p)) {
         switch (k) {
-#define LFM_K(K_) case K_: return launch_band2<FAM, K_>(p, grid, st);
+#define LFM_K(K_) case K_: return launch_band2<FAM, K_>(p, grid, st, ctl);
         LFM_K(1) LFM_K(2) LFM_K(3) LFM_K(4) LFM_K(5) LFM_K(6) LFM_K(7)
 #undef LFM_K
         default: return hipErrorInvalidValue;
@@ -804,19 +946,17 @@ static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st)
     return hipGetLastError();
 }
 
-} // namespace lfm
-
-// (checks that compile this file for one kernel define LFM_UNPREDICT_NO_ENTRY:
-// the entry point below instantiates every kernel)
-#ifndef LFM_UNPREDICT_NO_ENTRY
-extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
-                                 int nframes, int T, int family, int predictor, int video_bit, int z0, void* stream_)
+// Queues the inverse of every frame on `st`; with a control block (band5
+// shapes) its status word is copied into *h_status behind the kernels (the
+// caller reads it once the stream has passed that point), else *h_status = 0.
+static int unpredict_issue(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H, int nframes,
+                           int T, int family, int predictor, int video_bit, int z0, int* h_status, hipStream_t st)
 {
-    hipStream_t st = (hipStream_t)stream_;
     if (W <= 0 || H <= 0 || nframes <= 0 || T <= 0 || T > 31 || predictor < 0 || predictor > 7 || family < 0 ||
         family > 2)
         return LFM_HIP_EINVAL;
     const size_t bytes = (size_t)W * H * nframes * sizeof(uint16_t);
+    if (h_status) *h_status = 0;
     if (predictor == 0)
         return hipMemcpyAsync(d_out, d_sym, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess ? LFM_HIP_OK
                                                                                               : LFM_HIP_ERUNTIME;
@@ -824,25 +964,95 @@ extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, 
     const bool any_temporal = video && (nframes > 1 || (z0 & 1));
     if (any_temporal && family != 0) return LFM_HIP_ENOTINV;  // ((I - pred) + P) >> 1 drops a bit
     if (video && (z0 & 1) && !d_prev) return LFM_HIP_EINVAL;
-    lfm::UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, lfm::kSpinLimit, nullptr};
+    UnFrames p{d_sym, d_prev, d_out, W, H, T, nframes, z0, video, 0, 1, INT_MAX, 0u, nullptr, wait_ticks(), 0};
+    CtlBlock* ctl = nullptr;
+    if (band2_ok(p) && band4_waves(p)) {
+        const int nbands = (H + 63) / 64;
+        ctl = ctl_acquire((size_t)kCtlPos + (size_t)nframes * nbands);
+        if (!ctl) return LFM_HIP_ERUNTIME;
+        if (hipMemsetAsync(ctl->d, 0, sizeof(int), st) != hipSuccess) {
+            ctl_release(ctl, st);
+            return LFM_HIP_ERUNTIME;
+        }
+    }
     // without video every frame is spatial: one launch; with video the
     // spatial (even global z) frames first, then the temporal ones on their
     // decoded predecessors
     const int passes = video ? 2 : 1;
-    for (int pass = 0; pass < passes; ++pass) {
+    int rc = LFM_HIP_OK;
+    for (int pass = 0; pass < passes && rc == LFM_HIP_OK; ++pass) {
         if (video) {
             const int want = pass;  // global parity decoded by this pass
             p.first = (z0 & 1) == want ? 0 : 1;
             p.step = 2;
         }
         hipError_t e = hipErrorInvalidValue;
+        int* c = ctl ? ctl->d : nullptr;
         switch (family) {
-        case 0: e = lfm::launch_unpredict<0>(predictor, p, st); break;
-        case 1: e = lfm::launch_unpredict<1>(predictor, p, st); break;
-        case 2: e = lfm::launch_unpredict<2>(predictor, p, st); break;
+        case 0: e = lfm::launch_unpredict<0>(predictor, p, st, c); break;
+        case 1: e = lfm::launch_unpredict<1>(predictor, p, st, c); break;
+        case 2: e = lfm::launch_unpredict<2>(predictor, p, st, c); break;
         }
-        if (e != hipSuccess) return LFM_HIP_ERUNTIME;
+        if (e != hipSuccess) rc = LFM_HIP_ERUNTIME;
     }
-    return LFM_HIP_OK;
+    if (ctl) {
+        if (rc == LFM_HIP_OK && h_status &&
+            hipMemcpyAsync(h_status, ctl->d, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess)
+            rc = LFM_HIP_ERUNTIME;
+        ctl_release(ctl, st);
+    }
+    return rc;
+}
+
+} // namespace lfm
+
+// (checks that compile this file for one kernel define LFM_UNPREDICT_NO_ENTRY:
+// the entry points below instantiate every kernel)
+#ifndef LFM_UNPREDICT_NO_ENTRY
+extern "C" int lfm_hip_unpredict_check(int status)
+{
+    if (!status) return LFM_HIP_OK;
+    // without the band4 re-run (LFM_UNPREDICT_FALLBACK=0) a band5 timeout
+    // leaves pixels decoded from rows that were not ready
+    const bool fixed = (status & lfm::kStBand5) && !(status & (lfm::kStBand4)) && lfm::fallback_enabled();
+    std::fprintf(stderr, "lfm: inverse predictor band hand-over timed out (%s)%s\n",
+                 (status & lfm::kStBand4) ? "band4" : "band5",
+                 fixed ? "; frames re-run through band4" : "; the decoded pixels are not valid");
+    return fixed ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
+}
+
+extern "C" int lfm_hip_unpredict_async(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
+                                       int nframes, int T, int family, int predictor, int video_bit, int z0,
+                                       int* h_status, void* stream_)
+{
+    if (!h_status) return LFM_HIP_EINVAL;
+    const int rc = lfm::unpredict_issue(d_sym, d_prev, d_out, W, H, nframes, T, family, predictor, video_bit, z0,
+                                        h_status, (hipStream_t)stream_);
+    // (the caller passes the status word, once the stream is past the copy,
+    // to lfm_hip_unpredict_check)
+    return rc;
+}
+
+extern "C" int lfm_hip_unpredict(const uint16_t* d_sym, const uint16_t* d_prev, uint16_t* d_out, int W, int H,
+                                 int nframes, int T, int family, int predictor, int video_bit, int z0, void* stream_)
+{
+    hipStream_t st = (hipStream_t)stream_;
+    int* hs = nullptr;  // pinned, per thread (the copy behind the kernels lands there)
+    thread_local struct Pinned {
+        int* p = nullptr;
+        ~Pinned()
+        {
+            if (p) (void)hipHostFree(p);
+        }
+    } pin;
+    if (!pin.p && hipHostMalloc((void**)&pin.p, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        pin.p = nullptr;
+        return LFM_HIP_ERUNTIME;
+    }
+    hs = pin.p;
+    const int rc = lfm::unpredict_issue(d_sym, d_prev, d_out, W, H, nframes, T, family, predictor, video_bit, z0, hs, st);
+    if (rc != LFM_HIP_OK) return rc;
+    if (hipStreamSynchronize(st) != hipSuccess) return LFM_HIP_ERUNTIME;
+    return lfm_hip_unpredict_check(*hs);
 }
 #endif

@@ -39,7 +39,8 @@ EXPORTS = [
     "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab", "lfm_encoder_submit",
     "lfm_encoder_submit_select", "lfm_encoder_wait",
     # lfm_hip.h
-    "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
+    "lfm_hip_predict", "lfm_hip_unpredict", "lfm_hip_unpredict_async", "lfm_hip_unpredict_check",
+    "lfm_hip_predict_candidates", "lfm_hip_entropy2d", "lfm_hip_select_workspace_bytes", "lfm_hip_select",
     "lfm_hip_synth", "lfm_hip_device_count", "lfm_hip_force_generic", "lfm_hip_bzip2_workspace_bytes",
     "lfm_hip_bzip2_blocks", "lfm_hip_bzip2_last_stage_ms", "lfm_hip_bunzip2_workspace_bytes", "lfm_hip_bunzip2_blocks", "lfm_hip_scatter_blocks",
 ]

@@ -49,6 +49,9 @@ static void check(bool ok, const char* what)
 
 int main(int argc, char** argv)
 {
+    // line-buffered: a caller that kills this program still sees every check
+    // printed before the kill (stdout is a pipe under the tests)
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);
     if (argc != 8) {
         std::fprintf(stderr, "usage: %s input.u16 X Y Z outdir request video\n", argv[0]);
         return 2;

@@ -27,6 +27,7 @@ def _run(tmp_path, img, request, video):
     r = subprocess.run([EXE, str(raw), str(X), str(Y), str(Z), str(tmp_path), str(request), str(video)],
                        capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
+    assert "timed out" not in r.stderr, r.stderr  # (no inverse-predictor hand-over gave up)
     return (tmp_path / "klb.lfm").read_bytes(), (tmp_path / "mex.lfm").read_bytes()
 
 

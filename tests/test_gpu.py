@@ -504,6 +504,69 @@ def test_unpredict_rejects_lossy_temporal(lfmlib, gpu):
         lfmlib.unpredict_device(d, d.clone(), 16, 16, 2, 13, "angle", 4, video=1)
 
 
+@pytest.mark.parametrize("nfr", [1, 2, 3, 4, 5, 6, 7, 12])
+def test_unpredict_band5_frame_counts(lfmlib, oracle, gpu, nfr):
+    """The cross-workgroup inverse (band5: one single-wave workgroup per 64-row
+    band, 5 bands of a 520 x 300 tiles frame) for every frame count, above all
+    the counts that are not a multiple of 8 -- the round-5 hand-over timeout
+    (GPUTEST_r05: 4 frames x 5 bands) came from such a launch.  Bands take
+    their index from a ticket, not from blockIdx, so no count depends on the
+    dispatch order or the XCD placement; the pixels are exact and no
+    hand-over timed out (the call raises when one was not repaired)."""
+    import time
+    torch = gpu
+    stack = oracle.synthetic_lf(520, 300, Z=nfr, T=13, seed=0x4C464D09 + nfr)[0, 0]
+    for video in (0, 1):
+        sym = oracle.predict_volume(stack, 13, "tiles", 5, video)
+        d_sym = dev16(torch, sym)
+        d_out = torch.empty_like(d_sym)
+        t0 = time.time()
+        for _ in range(3):  # repeated on the same control blocks
+            d_out.zero_()
+            lfmlib.unpredict_device(d_sym, d_out, 520, 300, nfr, 13, "tiles", 5, video=video)
+            torch.cuda.synchronize()
+            assert np.array_equal(host16(d_out), stack), (nfr, video)
+        assert time.time() - t0 < 10.0
+
+
+def test_unpredict_forced_timeout_is_bounded(lfmlib, oracle, gpu, capfd, monkeypatch):
+    """A band5 hand-over forced to give up after one poll (LFM_UNPREDICT_SPIN=1)
+    on a frame count that is not a multiple of 8: every band stops waiting
+    once the status word carries the timeout, the device re-runs the frames
+    through band4, and the call returns exact pixels within a second,
+    reporting the timeout on stderr.  With LFM_UNPREDICT_FALLBACK=0 the same
+    call fails instead of returning the pixels."""
+    import time
+    torch = gpu
+    stack = oracle.synthetic_lf(520, 300, Z=4, T=13, seed=5)[0, 0]
+    sym = oracle.predict_volume(stack, 13, "tiles", 5, 0)
+    d_sym = dev16(torch, sym)
+    d_out = torch.empty_like(d_sym)
+    lfmlib.unpredict_device(d_sym, d_out, 520, 300, 4, 13, "tiles", 5)  # warm (module load)
+    torch.cuda.synchronize()
+    capfd.readouterr()
+    monkeypatch.setenv("LFM_UNPREDICT_SPIN", "1")
+    d_out.zero_()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    lfmlib.unpredict_device(d_sym, d_out, 520, 300, 4, 13, "tiles", 5)
+    dt = time.time() - t0
+    assert "hand-over timed out" in capfd.readouterr().err
+    assert dt < 1.0, dt
+    assert np.array_equal(host16(d_out), stack)
+    monkeypatch.setenv("LFM_UNPREDICT_FALLBACK", "0")
+    t0 = time.time()
+    with pytest.raises(lfmlib.LfmError):
+        lfmlib.unpredict_device(d_sym, d_out, 520, 300, 4, 13, "tiles", 5)
+    assert time.time() - t0 < 1.0
+    monkeypatch.delenv("LFM_UNPREDICT_SPIN")
+    monkeypatch.delenv("LFM_UNPREDICT_FALLBACK")
+    lfmlib.unpredict_device(d_sym, d_out, 520, 300, 4, 13, "tiles", 5)
+    torch.cuda.synchronize()
+    assert np.array_equal(host16(d_out), stack)
+    assert "timed out" not in capfd.readouterr().err
+
+
 def test_decode_roundtrip_through_gpu(lfmlib, oracle, gpu, tmp_path):
     """write (GPU predictor + GPU bzip2) -> read (bzip2 decode + GPU inverse)
     restores every pixel, video tiles stack included."""
