@@ -9,33 +9,53 @@
 // P = h / S in float.  Candidate 0 (raw) is scaled by 0.96; the argmin takes
 // the highest index on exact ties (std::map<float,int> overwrite).
 //
-// gfx950 pipeline, all candidates x chunks ("jobs") of one frame batched in
+// The sorted array L is never built.  In L the element after (key k, val
+// c[i-1]) is the next element of the same key in index order -- the next
+// occurrence i' > i of byte k, whose val is c[i'-1] -- or, for the last
+// element of a key, the first element of the next non-empty key (the
+// sentinel closes key 0).  So each position i has a PARTNER byte p[i], its
+// bigram is bin (c[i-1] << 8) | p[i], and the histogram is a position-order
+// pass over (c, p).  All candidates x chunks ("jobs") of a frame go through
 // every launch (the reference runs 3 kernels + a CUB radix sort + a blocking
-// thrust::reduce per candidate and chunk, serialised on the default stream):
-//   count   : per 4 KiB segment, key histogram (LDS)
-//   scan    : per job, bucket bases (sentinel closes bucket 0) + per-segment
-//             offsets
-//   scatter : stable counting sort, one wave per segment; in-wave stable rank
-//             from eight 64-bit ballots (peer mask), running counts in LDS
-//   bigram  : per 30720-pair slice, staged in LDS, 65536 16-bit counters
-//             packed in 128 KiB LDS (cannot overflow), run-length
-//             pre-aggregation per thread, non-zero bins added to the job's
-//             histogram with global atomics
-//   entropy : per job, -P logf P per bin in parallel, then fixed-order row
-//             sums and wave butterflies (deterministic)
+// thrust::reduce per candidate and chunk):
+//   ent_next : per 16 KiB segment (4 waves x 4 KiB): each wave walks its
+//              bytes backward in 64-position windows; a position's partner is
+//              the val of the next lane with the same byte (peer masks from
+//              eight ballots) or the first val of that byte in the later
+//              windows (a 256-entry LDS table); the four waves are linked the
+//              same way; per segment and byte: first val and last position
+//   ent_link : per job, per byte (one thread each): links the segments
+//              (last position of a segment <- first val of the byte in the
+//              later segments) and the keys (the last element of key k <-
+//              the first val of the next non-empty key; key 0's last element
+//              <- the sentinel's val; the sentinel <- key >= 1's first val);
+//              the one element without a partner (end of L) is recorded
+//   ent_rows : per (job, quarter of the rows by val & 3): counts its bins --
+//              64 rows x 256 u32 counters in LDS, written by nobody else, so
+//              no 16-bit packing, no merge and no global atomics -- then the
+//              -P logf P terms and the ascending row sums of its 64 rows
+//   host     : per job the 256 row sums are combined in the oracle's fixed
+//              order (lfm_oracle.c lfmo_entropy_chunk: the 64 rows of a
+//              quarter by an xor butterfly, quarters left to right) -- the
+//              same float additions the round-1..5 ent_sum kernel did.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 #include "lfm_hip.h"
 
 namespace lfm {
 
 constexpr uint32_t kChunkPix = 450000;
 constexpr uint32_t kChunkBytes = 2 * kChunkPix;
-constexpr uint32_t kSeg = 4096;                                   // bytes per count/scatter segment
-constexpr uint32_t kSegMax = (kChunkBytes + kSeg - 1) / kSeg;     // 220
-constexpr uint32_t kLStride = (kChunkBytes + 1 + 255) & ~255u;
+constexpr uint32_t kSub = 4096;                                   // bytes per wave of ent_next
+constexpr uint32_t kSeg = 4 * kSub;                               // bytes per ent_next workgroup
+constexpr uint32_t kSegMax = (kChunkBytes + kSeg - 1) / kSeg;     // 55
+constexpr uint32_t kLStride = (kChunkBytes + 16 + 255) & ~255u;   // partner bytes per job (16-byte reads past S)
+constexpr uint32_t kNoVal = 0x100;                                // "no val" (a byte is < 256)
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;
+constexpr int kRow = 257;                                         // padded LDS row (u32 / float)
 
 struct Jobs {
     const uint8_t* cand[8];  // candidate buffers as bytes
@@ -53,118 +73,60 @@ __device__ __forceinline__ void job_span(const Jobs& J, int job, const uint8_t*&
     S = (uint32_t)(n * 2);
 }
 
-// ---------------------------------------------------------------- count --
-// one 4 KiB segment per workgroup, 16 bytes per thread from one 16-byte load
-__global__ __launch_bounds__(256) void ent_count(Jobs J, uint32_t* __restrict__ cnt)
+// 16 bytes of c at o (16-byte aligned), zeros past S (the last chunk of a
+// buffer may end anywhere)
+__device__ __forceinline__ uint4 load16(const uint8_t* c, uint32_t o, uint32_t S)
 {
-    __shared__ uint32_t h[256];
+    if (o + 16 <= S) return *(const uint4*)(c + o);  // chunk starts are 16-byte aligned (450000 px * 2 B)
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t t = 0; t < 16 && o + t < S; ++t) w[t >> 2] |= (uint32_t)c[o + t] << ((t & 3) * 8);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int j)
+{
+    const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
+    return (w >> ((j & 3) * 8)) & 0xFFu;
+}
+
+// ------------------------------------------------------------- ent_next --
+// tab[job][seg][k] = (last position of byte k in the segment + 1) | first
+// val of byte k in the segment << 20 (kNoVal: absent); 0 when absent.
+__global__ __launch_bounds__(256) void ent_next(Jobs J, uint8_t* __restrict__ part, uint32_t* __restrict__ tab)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t sbytes[4][kSub + 16];
+    __shared__ uint16_t nxt[4][256];   // first val of byte k in this wave's later windows
+    __shared__ uint32_t last[4][256];  // last position of byte k in this wave's bytes
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int job = blockIdx.y;
     const uint8_t* c;
     uint32_t S;
     job_span(J, job, c, S);
     const uint32_t s0 = blockIdx.x * kSeg;
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t i = s0 + threadIdx.x * 16;
-    if (i < S) {
-        uint32_t w[4];
-        const uint32_t m = min(16u, S - i);
-        if (m == 16) {
-            const uint4 v = *(const uint4*)(c + i);  // chunk starts are 16-byte aligned (450000 px * 2 B)
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        } else {
-            for (int q = 0; q < 4; ++q) w[q] = 0;
-            for (uint32_t t = 0; t < m; ++t) w[t >> 2] |= (uint32_t)c[i + t] << ((t & 3) * 8);
-        }
-        uint32_t zeros = 0;
+    if (s0 >= S) return;  // uniform for the block
+    uint8_t* pj = part + (size_t)job * kLStride;
+    const uint32_t b0 = s0 + wave * kSub;
+    const uint32_t len = b0 < S ? min(kSub, S - b0) : 0u;
+    uint8_t* sb = sbytes[wave] + 16;  // sb[-1] = c[b0 - 1]
+    for (int k = lane; k < 256; k += 64) {
+        nxt[wave][k] = kNoVal;
+        last[wave][k] = kNoPos;
+    }
+    if (len) {
 #pragma unroll
-        for (uint32_t t = 0; t < 16; ++t) {
-            const uint32_t b = (w[t >> 2] >> ((t & 3) * 8)) & 0xFFu;
-            if (t >= m) break;
-            if (b == 0) ++zeros;
-            else atomicAdd(&h[b], 1u);
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t o = (q * 64 + lane) * 16;
+            if (o < len) *(uint4*)(sb + o) = load16(c, b0 + o, S);
         }
-        if (zeros) atomicAdd(&h[0], zeros);
+        if (lane == 0) sb[-1] = b0 > 0 ? c[b0 - 1] : 0;
     }
-    __syncthreads();
-    // (plain stores: non-temporal ones here and in ent_scan gave no measurable
-    // gain, and in ent_scatter's byte scatter they doubled the selection time;
-    // profiles/r03_ab_nt_stores.txt)
-    cnt[((size_t)job * kSegMax + blockIdx.x) * 256 + threadIdx.x] = h[threadIdx.x];
-}
-
-// ----------------------------------------------------------------- scan --
-// offs[job][seg][k] = start of segment seg's key-k elements in L.
-__global__ __launch_bounds__(256) void ent_scan(Jobs J, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ offs,
-                                                uint8_t* __restrict__ L)
-{
-    __shared__ uint32_t tot[256];
-    const int job = blockIdx.x;
-    const uint8_t* c;
-    uint32_t S;
-    job_span(J, job, c, S);
-    const uint32_t nseg = (S + kSeg - 1) / kSeg;
-    const int k = threadIdx.x;
-    const uint32_t* cj = cnt + (size_t)job * kSegMax * 256;
-    uint32_t t = 0;
-    for (uint32_t s = 0; s < nseg; ++s) t += cj[s * 256 + k];
-    tot[k] = t + (k == 0 ? 1u : 0u);  // sentinel closes bucket 0
-    __syncthreads();
-    // exclusive scan over 256 keys (serial by thread 0 is 256 adds; keep it simple and exact)
-    __shared__ uint32_t base[256];
-    if (k == 0) {
-        uint32_t acc = 0;
-        for (int i = 0; i < 256; ++i) { base[i] = acc; acc += tot[i]; }
-    }
-    __syncthreads();
-    uint32_t acc = base[k];
-    uint32_t* oj = offs + (size_t)job * kSegMax * 256;
-    for (uint32_t s = 0; s < nseg; ++s) {
-        oj[s * 256 + k] = acc;
-        acc += cj[s * 256 + k];
-    }
-    if (k == 0) {
-        // sentinel (key 0, val c[S-1]) sits after every key-0 element
-        L[(size_t)job * kLStride + acc] = S ? c[S - 1] : 0;
-    }
-}
-
-// -------------------------------------------------------------- scatter --
-// One wave per 4 KiB segment.  The segment (and the byte before it) is staged
-// in LDS with 16-byte loads first, so the 64 rank rounds never wait on HBM.
-__global__ __launch_bounds__(256) void ent_scatter(Jobs J, const uint32_t* __restrict__ offs, uint8_t* __restrict__ L)
-{
-    __shared__ uint32_t run[4][256];
-    __shared__ __attribute__((aligned(16))) uint8_t seg_bytes[4][kSeg + 16];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int job = blockIdx.y;
-    const uint32_t seg = blockIdx.x * 4 + wave;
-    const uint8_t* c;
-    uint32_t S;
-    job_span(J, job, c, S);
-    const uint32_t s0 = seg * kSeg;
-    if (s0 >= S) return;  // whole wave leaves; no block barrier below
-    const uint32_t* oj = offs + ((size_t)job * kSegMax + seg) * 256;
-    for (int i = lane; i < 256; i += 64) run[wave][i] = oj[i];
-    const uint32_t e = min(S, s0 + kSeg);
-    uint8_t* sb = seg_bytes[wave] + 16;  // sb[-1] = c[s0 - 1]
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t o = (q * 64 + lane) * 16;
-        if (s0 + o + 16 <= e) {
-            *(uint4*)(sb + o) = *(const uint4*)(c + s0 + o);
-        } else {
-            for (uint32_t t = 0; t < 16; ++t) sb[o + t] = s0 + o + t < e ? c[s0 + o + t] : 0;
-        }
-    }
-    if (lane == 0) sb[-1] = s0 > 0 ? c[s0 - 1] : 0;
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    uint8_t* Lj = L + (size_t)job * kLStride;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t g = 0; g < e - s0; g += 64) {
-        const uint32_t i = g + lane;
-        const bool valid = s0 + i < e;
+    const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int g = (int)((len + 63) / 64) - 1; g >= 0; --g) {
+        const uint32_t i = (uint32_t)g * 64 + lane;
+        const bool valid = i < len;
         const uint32_t key = valid ? sb[i] : 0u;
         const uint32_t val = valid ? sb[(int)i - 1] : 0u;
         uint64_t peers = __ballot(valid);
@@ -174,123 +136,173 @@ __global__ __launch_bounds__(256) void ent_scatter(Jobs J, const uint32_t* __res
             const uint64_t bb = __ballot(bit);
             peers &= bit ? bb : ~bb;
         }
-        const uint32_t rank = __popcll(peers & lt);
-        const uint32_t before = valid ? run[wave][key] : 0u;
+        const uint64_t hi = peers & above;
+        const int src = hi ? (int)__builtin_ctzll(hi) : lane;
+        const uint32_t pv = (uint32_t)__shfl((int)val, src);
+        uint32_t pt = hi ? pv : (valid ? (uint32_t)nxt[wave][key] : 0u);
         __builtin_amdgcn_wave_barrier();
         if (valid) {
-            Lj[before + rank] = (uint8_t)val;
-            // the highest lane of each peer group advances the bucket
-            if ((peers >> lane) == 1ull) run[wave][key] = before + rank + 1;
+            // the lowest lane of a byte's group is that byte's first
+            // occurrence from here on; the highest with no later occurrence
+            // in this wave's bytes is the wave's last occurrence
+            if (!(peers & below)) nxt[wave][key] = (uint16_t)val;
+            if (pt == kNoVal) {
+                last[wave][key] = b0 + i;
+                pt = 0;  // (linked below or by ent_link)
+            }
+            pj[b0 + i] = (uint8_t)pt;
         }
         __builtin_amdgcn_wave_barrier();
     }
-}
-
-// --------------------------------------------------------------- bigram --
-// Workgroup (slice, job) counts the bigrams of kSlice consecutive pairs of L:
-// the slice is staged in LDS with 16-byte loads, every thread walks 60
-// consecutive pairs (run-length pre-aggregated: the long (0,0) runs of the
-// non-zero key buckets become one atomic), 65536 16-bit counters packed in
-// 128 KiB of LDS (kSlice < 65536: no overflow), then the non-zero counters are
-// added to the job's u32 histogram in HBM.
-constexpr uint32_t kBins = 65536;
-constexpr uint32_t kBigramThreads = 512;
-// 60 pairs per thread: thread ranges start 15 words apart (odd), so the byte
-// reads of a wave hit 64 distinct LDS banks; 128 KiB + 30 KiB of LDS
-constexpr uint32_t kPerThread = 60;
-constexpr uint32_t kSlice = kPerThread * kBigramThreads;
-
-__global__ __launch_bounds__(kBigramThreads) void ent_bigram(Jobs J, const uint8_t* __restrict__ L,
-                                                             uint32_t* __restrict__ hist)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t packed[];  // kBins / 2 words, then the slice bytes
-    uint8_t* sl = (uint8_t*)(packed + kBins / 2);
-    const int job = blockIdx.y;
-    const uint8_t* c;
-    uint32_t S;
-    job_span(J, job, c, S);
-    const uint32_t p0 = blockIdx.x * kSlice;
-    if (p0 >= S) return;  // uniform for the block
-    const uint32_t n = min(kSlice, S - p0);  // pairs p0 .. p0+n-1 use L[p0 .. p0+n]
-    const uint8_t* Lj = L + (size_t)job * kLStride;
-    // L job stride and p0 are multiples of 16: the staged span is 16-byte aligned
-    for (uint32_t o = threadIdx.x * 16; o < n + 1; o += kBigramThreads * 16)
-        *(uint4*)(sl + o) = *(const uint4*)(Lj + p0 + o);  // reads stay inside the L stride's slack
-    for (uint32_t w = threadIdx.x; w < kBins / 2; w += kBigramThreads) packed[w] = 0;
     __syncthreads();
-    const uint32_t a0 = threadIdx.x * kPerThread;
-    const uint32_t a1 = min(n, a0 + kPerThread);
-    uint32_t cur = 0xFFFFFFFFu, cnt = 0;
-    if (a0 < a1) {
-        uint32_t prev = sl[a0];
-        for (uint32_t j = a0; j < a1; ++j) {
-            const uint32_t nxt = sl[j + 1];
-            const uint32_t bin = (prev << 8) | nxt;
-            prev = nxt;
-            if (bin == cur) { ++cnt; continue; }
-            if (cnt) atomicAdd(&packed[cur >> 1], cnt << ((cur & 1) * 16));
-            cur = bin;
-            cnt = 1;
+    // link the four waves, byte k per thread: the last occurrence of k in a
+    // wave gets the first val of k in the waves after it
+    const int k = threadIdx.x;
+    uint32_t carry = kNoVal, seg_last = kNoPos;
+    for (int w = 3; w >= 0; --w) {
+        const uint32_t lp = last[w][k];
+        if (lp != kNoPos) {
+            if (carry == kNoVal) seg_last = lp;
+            else pj[lp] = (uint8_t)carry;
         }
-        if (cnt) atomicAdd(&packed[cur >> 1], cnt << ((cur & 1) * 16));
+        if (nxt[w][k] != kNoVal) carry = nxt[w][k];
     }
-    __syncthreads();
-    uint32_t* hj = hist + (size_t)job * kBins;
-    for (uint32_t w = threadIdx.x; w < kBins / 2; w += kBigramThreads) {
-        const uint32_t v = packed[w];
-        if (v & 0xFFFFu) atomicAdd(&hj[2 * w], v & 0xFFFFu);
-        if (v >> 16) atomicAdd(&hj[2 * w + 1], v >> 16);
-    }
+    tab[((size_t)job * kSegMax + blockIdx.x) * 256 + k] = seg_last == kNoPos ? 0u : ((seg_last + 1) | (carry << 20));
 }
 
-// -------------------------------------------------------------- entropy --
-// Per job: H = sum over bins b < 65535 of -P logf P, P = h / S, in the fixed
-// order the oracle restates (lfm_oracle.c lfmo_entropy_chunk): row r (bins
-// 256r .. 256r+255) summed in ascending order by one lane, the 64 rows of a
-// quarter combined by the wave's xor butterfly, quarters ((q0+q1)+q2)+q3.
-// The per-bin terms are formed by all threads into LDS first (they do not
-// depend on the order), then one wave runs the ordered row sums.
-constexpr int kRow = 257;
-__global__ __launch_bounds__(256) void ent_sum(Jobs J, const uint32_t* __restrict__ hist, float* __restrict__ ent)
+// ------------------------------------------------------------- ent_link --
+// meta[job] = {position whose element ends L (no bigram) or kNoPos,
+//              the sentinel's bin or kNoPos}
+__global__ __launch_bounds__(256) void ent_link(Jobs J, uint8_t* __restrict__ part, const uint32_t* __restrict__ tab,
+                                                uint32_t* __restrict__ meta)
 {
-    extern __shared__ float term[];  // 64 rows x kRow
-    __shared__ float quarter[4];
+    __shared__ uint32_t T[kSegMax * 256];
+    __shared__ uint32_t F[256], NF[256];
+    __shared__ uint32_t skip;
     const int job = blockIdx.x;
     const uint8_t* c;
     uint32_t S;
     job_span(J, job, c, S);
-    const float fs = (float)S;
-    const uint32_t* hj = hist + (size_t)job * kBins;
-    for (int q = 0; q < 4; ++q) {
-        for (uint32_t i = threadIdx.x; i < 16384; i += 256) {
-            const uint32_t b = q * 16384 + i;
-            const uint32_t h = hj[b];
-            float t = 0.f;
-            if (h && b != 0xFFFFu) {  // bin 0xFFFF is never summed by the reference
-                const float P = (float)h / fs;
-                t = -1.0f * P * logf(P);
-            }
-            term[(i >> 8) * kRow + (i & 255)] = t;
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {
-            const float* row = term + threadIdx.x * kRow;
-            float e = 0.f;
-            for (int k = 0; k < 256; ++k) e += row[k];
-            for (int off = 32; off > 0; off >>= 1) e += __shfl_xor(e, off);
-            if (threadIdx.x == 0) quarter[q] = e;
-        }
-        __syncthreads();
+    uint8_t* pj = part + (size_t)job * kLStride;
+    const uint32_t nseg = (S + kSeg - 1) / kSeg;
+    const uint32_t* tj = tab + (size_t)job * kSegMax * 256;
+    for (uint32_t o = threadIdx.x; o < nseg * 256; o += 256) T[o] = tj[o];
+    if (threadIdx.x == 0) skip = kNoPos;
+    __syncthreads();
+    const int k = threadIdx.x;
+    uint32_t carry = kNoVal, glast = kNoPos;
+    for (int s = (int)nseg - 1; s >= 0; --s) {
+        const uint32_t t = T[s * 256 + k];
+        if (!t) continue;
+        const uint32_t lp = (t & 0xFFFFFu) - 1;
+        if (carry == kNoVal) glast = lp;  // the last occurrence of k in the chunk
+        else pj[lp] = (uint8_t)carry;
+        carry = t >> 20;
     }
-    if (threadIdx.x == 0) ent[job] = ((quarter[0] + quarter[1]) + quarter[2]) + quarter[3];
+    F[k] = carry;  // first val of key k (kNoVal: k absent)
+    __syncthreads();
+    if (k == 0) {  // NF[k] = first val of the next non-empty key > k
+        uint32_t nf = kNoVal;
+        for (int q = 255; q >= 0; --q) {
+            NF[q] = nf;
+            if (F[q] != kNoVal) nf = F[q];
+        }
+    }
+    __syncthreads();
+    const uint32_t sval = S ? c[S - 1] : 0u;  // the sentinel (key 0) closes key 0
+    if (glast != kNoPos) {
+        const uint32_t p = k == 0 ? sval : NF[k];
+        if (p == kNoVal) skip = glast;  // the end of L (one key at most)
+        else pj[glast] = (uint8_t)p;
+    }
+    __syncthreads();
+    if (k == 0) {
+        meta[2 * job] = skip;
+        meta[2 * job + 1] = NF[0] == kNoVal ? kNoPos : ((sval << 8) | NF[0]);
+    }
+}
+
+// ------------------------------------------------------------- ent_rows --
+// Workgroup (job, quarter q) owns the 64 rows r = 4m + q (bins r * 256 ..
+// r * 256 + 255, r = the bigram's first byte): it counts them over every
+// position of the job, then writes the 64 row sums rows[job][r].  The
+// quarters of a job are blocks b, b + 8, b + 16, b + 24 (one XCD: the job's
+// bytes are read from one L2).  Bin 0 -- (0, 0), the high bytes of small
+// symbols -- is counted in registers.
+constexpr int kRowThreads = 512;
+__global__ __launch_bounds__(kRowThreads) void ent_rows(Jobs J, const uint8_t* __restrict__ part,
+                                                        const uint32_t* __restrict__ meta, float* __restrict__ rows)
+{
+    extern __shared__ uint32_t cnt[];  // 64 rows x kRow
+    __shared__ uint32_t zsum;
+    const int blk = blockIdx.x;
+    const int job = (blk >> 5) * 8 + (blk & 7), q = (blk >> 3) & 3;
+    if (job >= J.njobs) return;  // uniform for the block
+    const uint8_t* c;
+    uint32_t S;
+    job_span(J, job, c, S);
+    const uint8_t* pj = part + (size_t)job * kLStride;
+    for (int o = threadIdx.x; o < 64 * kRow; o += kRowThreads) cnt[o] = 0;
+    if (threadIdx.x == 0) zsum = 0;
+    const uint32_t skip = meta[2 * job], extra = meta[2 * job + 1];
+    __syncthreads();
+    uint32_t zeros = 0;
+    for (uint32_t i0 = threadIdx.x * 16; i0 < S; i0 += kRowThreads * 16) {
+        const uint4 pv = *(const uint4*)(pj + i0);  // (the stride holds 16 bytes past S)
+        const uint4 cv = load16(c, i0, S);
+        uint32_t prev = i0 ? c[i0 - 1] : 0u;  // c[-1] = 0
+        const uint32_t n = min(16u, S - i0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t val = prev, p = byte_of(pv, j);
+            prev = byte_of(cv, j);
+            const uint32_t i = i0 + j;
+            if ((uint32_t)j >= n || i == skip) continue;
+            const uint32_t bin = (val << 8) | p;
+            if (bin == 0) ++zeros;
+            else if ((val & 3u) == (uint32_t)q) atomicAdd(&cnt[(val >> 2) * kRow + p], 1u);
+        }
+    }
+    if (extra != kNoPos && threadIdx.x == 0 && ((extra >> 8) & 3u) == (uint32_t)q) {
+        if (extra == 0) ++zeros;
+        else atomicAdd(&cnt[(extra >> 10) * kRow + (extra & 0xFFu)], 1u);
+    }
+    if (q == 0) {
+        for (int off = 32; off > 0; off >>= 1) zeros += __shfl_xor(zeros, off);
+        if ((threadIdx.x & 63) == 0 && zeros) atomicAdd(&zsum, zeros);
+    }
+    __syncthreads();
+    if (q == 0 && threadIdx.x == 0) cnt[0] += zsum;
+    __syncthreads();
+    // -P logf P per bin in place (bin 0xFFFF is never summed by the
+    // reference), then row sums in ascending bin order
+    const float fs = (float)S;
+    float* term = (float*)cnt;
+    for (int o = threadIdx.x; o < 64 * 256; o += kRowThreads) {
+        const int m = o >> 8, b = o & 255;
+        const uint32_t bin = ((uint32_t)(4 * m + q) << 8) | (uint32_t)b;
+        const uint32_t h = cnt[m * kRow + b];
+        float t = 0.f;
+        if (h && bin != 0xFFFFu) {
+            const float P = (float)h / fs;
+            t = -1.0f * P * logf(P);
+        }
+        term[m * kRow + b] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const float* row = term + threadIdx.x * kRow;
+        float e = 0.f;
+        for (int b = 0; b < 256; ++b) e += row[b];
+        rows[(size_t)job * 256 + 4 * threadIdx.x + q] = e;
+    }
 }
 
 struct Workspace {
-    uint32_t* cnt;
-    uint32_t* offs;
-    uint8_t* L;
-    uint32_t* hist;
-    float* ent;
+    uint32_t* tab;
+    uint8_t* part;
+    uint32_t* meta;
+    float* rows;
     uint16_t* cands;  // 7 candidate buffers (select only)
 };
 
@@ -303,28 +315,39 @@ static size_t workspace_layout(uint64_t npix, int ncand, bool with_cands, Worksp
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += align256(bytes); return base ? base + o : nullptr; };
     uint8_t* p;
-    p = take(jobs * kSegMax * 256 * 4); if (w) w->cnt = (uint32_t*)p;
-    p = take(jobs * kSegMax * 256 * 4); if (w) w->offs = (uint32_t*)p;
-    p = take(jobs * (size_t)kLStride); if (w) w->L = p;
-    p = take(jobs * kBins * 4); if (w) w->hist = (uint32_t*)p;
-    p = take(jobs * 4); if (w) w->ent = (float*)p;
+    p = take(jobs * kSegMax * 256 * 4); if (w) w->tab = (uint32_t*)p;
+    p = take(jobs * (size_t)kLStride); if (w) w->part = p;
+    p = take(jobs * 8); if (w) w->meta = (uint32_t*)p;
+    p = take(jobs * 256 * 4); if (w) w->rows = (float*)p;
     p = take(with_cands ? (size_t)7 * npix * 2 : 0); if (w) w->cands = (uint16_t*)p;
     return off;
 }
 
 static hipError_t run_entropy(const Jobs& J, const Workspace& w, hipStream_t st)
 {
-    const uint32_t nsegBlocks = kSegMax;
-    hipError_t e = hipMemsetAsync(w.hist, 0, (size_t)J.njobs * kBins * 4, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ent_count, dim3(nsegBlocks, J.njobs), dim3(256), 0, st, J, w.cnt);
-    hipLaunchKernelGGL(ent_scan, dim3(J.njobs), dim3(256), 0, st, J, w.cnt, w.offs, w.L);
-    hipLaunchKernelGGL(ent_scatter, dim3((nsegBlocks + 3) / 4, J.njobs), dim3(256), 0, st, J, w.offs, w.L);
-    const uint32_t nslice = (kChunkBytes + kSlice - 1) / kSlice;
-    hipLaunchKernelGGL(ent_bigram, dim3(nslice, J.njobs), dim3(kBigramThreads), (kBins / 2) * 4 + kSlice + 16, st, J,
-                       w.L, w.hist);
-    hipLaunchKernelGGL(ent_sum, dim3(J.njobs), dim3(256), 64 * kRow * 4, st, J, w.hist, w.ent);
+    hipLaunchKernelGGL(ent_next, dim3(kSegMax, J.njobs), dim3(256), 0, st, J, w.part, w.tab);
+    hipLaunchKernelGGL(ent_link, dim3(J.njobs), dim3(256), 0, st, J, w.part, w.tab, w.meta);
+    const uint32_t nblk = (uint32_t)((J.njobs + 7) / 8) * 32;
+    hipLaunchKernelGGL(ent_rows, dim3(nblk), dim3(kRowThreads), 64 * kRow * 4, st, J, w.part, w.meta, w.rows);
     return hipGetLastError();
+}
+
+// the oracle's fixed order (lfm_oracle.c lfmo_entropy_chunk) over one job's
+// 256 row sums: the 64 rows of a quarter by an xor butterfly, then the
+// quarters left to right
+static float combine_rows(const float* part)
+{
+    float w[4];
+    for (int q = 0; q < 4; ++q) {
+        float v[64], nv[64];
+        for (int l = 0; l < 64; ++l) v[l] = part[q * 64 + l];
+        for (int off = 32; off > 0; off >>= 1) {
+            for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+            std::memcpy(v, nv, sizeof(v));
+        }
+        w[q] = v[0];
+    }
+    return ((w[0] + w[1]) + w[2]) + w[3];
 }
 
 } // namespace lfm
@@ -342,17 +365,16 @@ static int entropy_impl(const uint16_t* const* cands, int ncand, uint64_t npix, 
     Workspace w{};
     workspace_layout(npix, ncand, false, &w, (uint8_t*)dws);
     if (run_entropy(J, w, st) != hipSuccess) return LFM_HIP_ERUNTIME;
-    float* h_ent = (float*)malloc(sizeof(float) * J.njobs);
-    hipError_t e = hipMemcpyAsync(h_ent, w.ent, sizeof(float) * J.njobs, hipMemcpyDeviceToHost, st);
+    std::vector<float> h_rows((size_t)J.njobs * 256);
+    hipError_t e = hipMemcpyAsync(h_rows.data(), w.rows, h_rows.size() * sizeof(float), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess) {
         for (int k = 0; k < ncand; ++k) {
             float acc = 0.f;  // entropy_A += per-chunk reduce, in chunk order
-            for (int q = 0; q < J.nchunks; ++q) acc += h_ent[k * J.nchunks + q];
+            for (int q = 0; q < J.nchunks; ++q) acc += combine_rows(h_rows.data() + (size_t)(k * J.nchunks + q) * 256);
             out[k] = acc;
         }
     }
-    free(h_ent);
     (void)own_ws;
     return e == hipSuccess ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
 }

@@ -946,6 +946,9 @@ static hipError_t launch_unpredict(int k, const UnFrames& p, hipStream_t st, int
     return hipGetLastError();
 }
 
+// (checks that compile this file for one kernel define LFM_UNPREDICT_NO_ENTRY:
+// unpredict_issue and the entry points below instantiate every kernel)
+#ifndef LFM_UNPREDICT_NO_ENTRY
 // Queues the inverse of every frame on `st`; with a control block (band5
 // shapes) its status word is copied into *h_status behind the kernels (the
 // caller reads it once the stream has passed that point), else *h_status = 0.
@@ -1003,11 +1006,10 @@ static int unpredict_issue(const uint16_t* d_sym, const uint16_t* d_prev, uint16
     }
     return rc;
 }
+#endif
 
 } // namespace lfm
 
-// (checks that compile this file for one kernel define LFM_UNPREDICT_NO_ENTRY:
-// the entry points below instantiate every kernel)
 #ifndef LFM_UNPREDICT_NO_ENTRY
 extern "C" int lfm_hip_unpredict_check(int status)
 {

@@ -162,6 +162,30 @@ def test_entropy_single_candidate(lfmlib, oracle, gpu):
         assert abs(e - oracle.entropy2d(cand)) <= 1e-5 * max(1.0, abs(e)), hex(v)
 
 
+@pytest.mark.parametrize("dist", ["small", "bytes", "few", "runs"])
+def test_entropy_partner_links(lfmlib, oracle, gpu, dist):
+    """The selection never builds the sorted pair array: every position's
+    bigram partner is the next occurrence of its byte, linked across the
+    64-position windows, the four 4 KiB waves and the 16 KiB segments of
+    ent_next, then across keys (sentinel, end of L) by ent_link.  Sizes put
+    those seams and the chunk / 16-byte tails in every position; the value
+    distributions leave keys absent, make one key hold everything, or make
+    long runs."""
+    torch = gpu
+    rng = np.random.default_rng({"small": 1, "bytes": 2, "few": 3, "runs": 4}[dist])
+    for n in (1, 2, 8, 9, 31, 32, 33, 2047, 2048, 2049, 8191, 8192, 8193, 24577, 449999, 450000, 450007):
+        if dist == "small":
+            cand = np.abs(rng.normal(0, 40, size=n)).astype(np.uint16)
+        elif dist == "bytes":
+            cand = rng.integers(0, 65536, size=n, dtype=np.uint16)
+        elif dist == "few":
+            cand = rng.choice(np.array([0x0100, 0x0302, 0x0001], np.uint16), size=n)
+        else:
+            cand = np.repeat(rng.integers(0, 6, size=n // 50 + 1, dtype=np.uint16), 50)[:n]
+        e = lfmlib.entropy_device(dev16(torch, cand))
+        assert abs(e - oracle.entropy2d(cand)) <= 1e-5 * max(1.0, abs(e)), (dist, n)
+
+
 def _manifest():
     return {e["name"]: e for e in json.load(open(os.path.join(GOLDEN, "lfm_manifest.json")))}
 
