@@ -25,7 +25,12 @@ extern "C" {
 
 LFM_API int lfm_set_family(int family);
 LFM_API int lfm_get_family(void);
+/* Interface version of this header (also in lfm_version()'s string).
+ * 2: lfm_decode_memory_roi takes out_bytes before numThreads (round 5; a
+ *    caller built against version 1 passed numThreads third-to-last). */
+#define LFM_API_VERSION 2
 LFM_API const char* lfm_version(void);
+LFM_API int lfm_api_version(void);
 
 /* predictor_request: header bits 0-6 (0..7 auto, 8..15 forced k = request-8);
  * video: header bit 7.  Returns the writeKLBstack codes. */

@@ -24,7 +24,8 @@ extern "C" int lfm_set_family(int family)
     return 0;
 }
 extern "C" int lfm_get_family(void) { return lfm::current_family(); }
-extern "C" const char* lfm_version(void) { return "lfm-mi355x 0.1 (gfx950)"; }
+extern "C" const char* lfm_version(void) { return "lfm-mi355x 0.2 (gfx950, api 2)"; }
+extern "C" int lfm_api_version(void) { return LFM_API_VERSION; }
 
 extern "C" int writeLFMstack_c(const void* im, const char* filename, const uint32_t xyzct[KLB_DATA_DIMS],
                                int dataType, int numThreads, const float pixelSize[KLB_DATA_DIMS],

@@ -3698,13 +3698,23 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
     // still queued): a caller may start its next work beside this tail
     // (earlier, after the second or third code-length round, measured slower:
     // the next encode's kernels then slow these latency-bound rounds)
-    static thread_local hipEvent_t ev_tables = nullptr;
-    static thread_local int ev_tables_dev = -1;
-    if (t_hook && ev_tables_dev != dev) {
-        if (ev_tables) (void)hipEventDestroy(ev_tables);
-        ev_tables = nullptr;
-        if (hipEventCreateWithFlags(&ev_tables, hipEventDisableTiming) == hipSuccess) ev_tables_dev = dev;
+    // (one per thread, destroyed when the thread exits: gpu_compress starts
+    // its slot threads per call)
+    static thread_local struct TablesEvent {
+        hipEvent_t ev = nullptr;
+        int dev = -1;
+        ~TablesEvent()
+        {
+            if (ev) (void)hipEventDestroy(ev);
+        }
+    } tables_ev;
+    if (t_hook && tables_ev.dev != dev) {
+        if (tables_ev.ev) (void)hipEventDestroy(tables_ev.ev);
+        tables_ev.ev = nullptr;
+        tables_ev.dev = -1;
+        if (hipEventCreateWithFlags(&tables_ev.ev, hipEventDisableTiming) == hipSuccess) tables_ev.dev = dev;
     }
+    hipEvent_t ev_tables = tables_ev.ev;
     for (int it = 0; it < kIters; ++it) {
         hipLaunchKernelGGL(huff_select_reg, dim3(count), dim3(kHuffThreads), 0, st, B);
         // uniform heaps, 32 per workgroup: u32 entries for the narrow tables,

@@ -202,7 +202,9 @@ int MemSink::append(const uint8_t* p, size_t n)
 uint8_t* MemSink::direct(size_t n)
 {
     const size_t at = out_->size();
-    if (at + n > out_->capacity() && worst_ > at + n && !out_->reserve(worst_)) return nullptr;
+    // grow once to the worst case; if that reservation fails, the plain
+    // resize below still grows by what this append needs
+    if (at + n > out_->capacity() && worst_ > at + n) (void)out_->reserve(worst_);
     if (!out_->resize(at + n)) return nullptr;
     return out_->data() + at;
 }

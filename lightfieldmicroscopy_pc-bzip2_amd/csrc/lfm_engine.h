@@ -94,7 +94,9 @@ public:
     // fits): a 100-volume config-5 stack (107 GB raw, 52 GB .lfm) would
     // otherwise pin 110 GB of host memory for its output.  A stack that
     // compresses worse grows the buffer once, straight to the worst case
-    // (direct()), so the peak is the old buffer plus n, never more.
+    // (direct()): the peak is the old buffer plus n, 1.6 n; if n cannot be
+    // pinned, the buffer grows by half its capacity at a time instead (first
+    // step: 0.6 n + 0.9 n = 1.5 n).
     void reserve_hint(size_t n) override
     {
         const size_t big = (size_t)8 << 30;

@@ -33,7 +33,7 @@ EXPORTS = [
     "writeKLBstack", "writeKLBstackSlices", "readKLBheader", "readKLBstack", "readKLBstackInPlace",
     "readKLBroiInPlace",
     # lfm_api.h
-    "lfm_set_family", "lfm_get_family", "lfm_version", "writeLFMstack_c", "readLFMstack_c",
+    "lfm_set_family", "lfm_get_family", "lfm_version", "lfm_api_version", "writeLFMstack_c", "readLFMstack_c",
     "lfm_encoder_create", "lfm_encoder_destroy", "lfm_encoder_encode", "lfm_encoder_encode_slab",
     "lfm_merge_slabs", "lfm_free", "lfm_decode_memory", "lfm_decode_memory_roi", "lfm_set_devices", "lfm_get_devices", "lfm_default_devices",
     "lfm_encoder_encode_multi", "lfm_release_encoders", "lfm_slab_info", "lfm_place_slab", "lfm_encoder_submit",
@@ -89,6 +89,8 @@ def lib():
     L.readKLBstackInPlace.argtypes = [ctypes.c_char_p, vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.readKLBroiInPlace.argtypes = [ctypes.c_char_p, vp, u32p, u32p, ctypes.c_int]
     L.lfm_version.restype = ctypes.c_char_p
+    if L.lfm_api_version() != 2:  # lfm_decode_memory_roi's argument list (lfm_api.h)
+        raise OSError("liblfm.so API version %d, this binding needs 2" % L.lfm_api_version())
     L.writeLFMstack_c.argtypes = [vp, ctypes.c_char_p, u32p, ctypes.c_int, ctypes.c_int, f32p, u32p, ctypes.c_int,
                                   ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.readLFMstack_c.argtypes = [ctypes.c_char_p, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint8),
