@@ -73,21 +73,20 @@ struct UnFrames {
     uint16_t* out;         // nz decoded frames
     int W, H, T, nz, z0, video;
     int first, step;       // this launch decodes local frames first, first + step, ...
-    // band4 / band5 hand-over: a wait gives up after wait_ticks of the
-    // 100 MHz real-time clock (or spin_limit polls: tests force a timeout),
-    // ORs err_bit into *status (global memory) and from then on every wait of
-    // that band returns at once; a band5 wait also gives up as soon as any
-    // other band has set the bit.  The launch that follows a band5 launch
-    // (band4, `repair`) re-runs every frame when bit 1 is set.
+    // band5 hand-over: a wait gives up after wait_ticks of the 100 MHz
+    // real-time clock (or spin_limit polls: tests force a timeout), ORs
+    // err_bit into *status (global memory) and from then on every wait of
+    // that band returns at once; it also gives up as soon as any other band
+    // has set the bit.  The launch that follows a band5 launch (the one-wave
+    // kernel, `repair`) re-runs every frame when the bit is set.
     int spin_limit;
     unsigned err_bit;
     unsigned* status;
     uint64_t wait_ticks;
-    int repair;            // band4 only: run only if a band5 hand-over gave up
+    int repair;            // unpredict_band only: run only if a band5 hand-over gave up
 };
 // status bits (the control block's word 0, reported to the caller)
-constexpr unsigned kStBand5 = 1u;   // a band5 hand-over timed out (frames re-run through band4)
-constexpr unsigned kStBand4 = 2u;   // a band4 hand-over timed out: the pixels are not valid
+constexpr unsigned kStBand5 = 1u;   // a band5 hand-over timed out (the frames are re-run)
 // control block (hipMalloc'd, pooled): word 0 status, word 32 the band5
 // ticket counter, words 33.. the band progress words (0 before the launch)
 constexpr int kCtlTicket = 32, kCtlPos = 33;
@@ -98,6 +97,10 @@ __global__ __launch_bounds__(64) void unpredict_band(UnFrames p)
     __shared__ uint16_t ring[64 * kRing];
     const int fz = p.first + (int)blockIdx.x * p.step;
     if (fz >= p.nz) return;
+    // the re-run after a band5 launch (one wave per frame, 8 KiB of LDS, so
+    // it is dispatched at once beside other work): nothing to do unless one
+    // of that launch's hand-overs gave up
+    if (p.repair && !(__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStBand5)) return;
     const int r = threadIdx.x;
     const size_t fs = (size_t)p.W * p.H;
     const uint16_t* sym = p.sym + fz * fs;
@@ -456,8 +459,8 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
     const int W = p.W, H = p.H, T = p.T, TT = T + 1;
     const int nbands = (H + 63) / 64, kend = W + 63, stride = W + 64 + 3 * kSync;
     const int prodw = (wv + NW - 1) % NW;
-    // (bounded in time: a wait that gives up sets its bit in *p.status -- a
-    // band5 launch is then re-run through band4 on the device -- and the band
+    // (bounded in time: a wait that gives up sets its bit in *p.status -- the
+    // frames of a band5 launch are then re-run on the device -- and the band
     // runs on without waiting; never a hang.)  Progress is monotonic, so a
     // stale read can only under-report it: it delays a band, never releases
     // one early.
@@ -680,26 +683,6 @@ __device__ __forceinline__ void band4(const UnFrames& p, int fz, int NW, int wv,
     }
 }
 
-template <int FAM, int K>
-__global__ __launch_bounds__(512) void unpredict_band4(UnFrames p, int NW)
-{
-    extern __shared__ __attribute__((aligned(16))) uint16_t lds4[];
-    __shared__ int pos[8];  // progress of each wave (band * stride + steps done)
-    const int fz = p.first + (int)blockIdx.x * p.step;
-    if (fz >= p.nz) return;
-    // the re-run after a band5 launch: nothing to do unless one of its
-    // hand-overs gave up (that launch's bit is in the status word)
-    if (p.repair && !(__hip_atomic_load(p.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kStBand5)) return;
-    const int wv = threadIdx.x >> 6, TT = p.T + 1;
-    if (threadIdx.x < (unsigned)NW) pos[threadIdx.x] = -1;
-    __syncthreads();
-    const int base = 0;
-    const int per = 64 * kRing + TT * kHand;
-    const int ring_off = base + wv * per, hand_off = ring_off + 64 * kRing;
-    if (p.video && ((p.z0 + fz) & 1)) band4<FAM, K, true>(p, fz, NW, wv, lds4, ring_off, hand_off, pos);
-    else band4<FAM, K, false>(p, fz, NW, wv, lds4, ring_off, hand_off, pos);
-}
-
 // band5: the band pipeline spread over the whole chip -- one single-wave
 // workgroup per (band, frame).  HIP promises neither a dispatch order nor a
 // workgroup -> XCD placement, so a workgroup does not take its band from
@@ -770,11 +753,11 @@ static int band4_waves(const UnFrames& p)
     return nw >= 2 ? nw : 0;
 }
 
-// Hand-over limits.  LFM_UNPREDICT_WAIT_MS (default 500): a band5 / band4 wait
+// Hand-over limits.  LFM_UNPREDICT_WAIT_MS (default 500): a band5 wait
 // gives up after that long on the device's 100 MHz real-time clock.
 // LFM_UNPREDICT_SPIN (tests): band5 waits give up after that many polls.
 // LFM_UNPREDICT_FALLBACK=0: a band5 timeout is reported as an error instead of
-// re-running the frames through band4.  Read per call (tests set them in the
+// re-running the frames.  Read per call (tests set them in the
 // process).
 static int band5_spin_limit()
 {
@@ -894,21 +877,18 @@ static hipError_t launch_band2(const UnFrames& p, int grid, hipStream_t st, int*
         }
         // re-run on the device, no host round trip: a band that gave up
         // decoded from rows that were not ready, so when the status word
-        // carries kStBand5 every frame of the launch runs again through band4
-        // (one workgroup per frame: its bands share one workgroup, so they are
-        // co-resident); otherwise its workgroups return at once
+        // carries kStBand5 every frame of the launch runs again through the
+        // one-wave kernel (a frame's bands are one wave's loop: nothing to
+        // wait for); otherwise its waves return at once.  (The round-5 re-run
+        // was band4 -- 512 threads and up to 129 KiB of LDS per frame -- whose
+        // launch waited up to 9 ms for CUs held by the other decode slot's
+        // bzip2 kernels even when it had nothing to do.)
         if (e == hipSuccess && fallback_enabled()) {
-            const int nw = band4_waves(p);
-            const size_t lds4 = (size_t)nw * (64 * kRing + (p.T + 1) * kHand) * 2;
-            const void* fn4 = (const void*)unpredict_band4<FAM, K_>;
-            if (hipFuncSetAttribute(fn4, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds4) != hipSuccess)
-                return hipErrorInvalidValue;
             UnFrames pr = p;
             pr.status = (unsigned*)ctl;
-            pr.err_bit = kStBand4;
-            pr.spin_limit = INT_MAX;
+            pr.err_bit = 0;
             pr.repair = 1;
-            hipLaunchKernelGGL((unpredict_band4<FAM, K_>), dim3(grid), dim3(64 * nw), lds4, st, pr, nw);
+            hipLaunchKernelGGL((unpredict_band<FAM, K_>), dim3(grid), dim3(64), 0, st, pr);
             e = hipGetLastError();
         }
         return e;
@@ -1014,12 +994,11 @@ static int unpredict_issue(const uint16_t* d_sym, const uint16_t* d_prev, uint16
 extern "C" int lfm_hip_unpredict_check(int status)
 {
     if (!status) return LFM_HIP_OK;
-    // without the band4 re-run (LFM_UNPREDICT_FALLBACK=0) a band5 timeout
-    // leaves pixels decoded from rows that were not ready
-    const bool fixed = (status & lfm::kStBand5) && !(status & (lfm::kStBand4)) && lfm::fallback_enabled();
-    std::fprintf(stderr, "lfm: inverse predictor band hand-over timed out (%s)%s\n",
-                 (status & lfm::kStBand4) ? "band4" : "band5",
-                 fixed ? "; frames re-run through band4" : "; the decoded pixels are not valid");
+    // without the re-run (LFM_UNPREDICT_FALLBACK=0) a band5 timeout leaves
+    // pixels decoded from rows that were not ready
+    const bool fixed = status == (int)lfm::kStBand5 && lfm::fallback_enabled();
+    std::fprintf(stderr, "lfm: inverse predictor band hand-over timed out (band5)%s\n",
+                 fixed ? "; frames re-run by the one-wave kernel" : "; the decoded pixels are not valid");
     return fixed ? LFM_HIP_OK : LFM_HIP_ERUNTIME;
 }
 

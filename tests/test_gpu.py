@@ -566,7 +566,7 @@ def test_unpredict_forced_timeout_is_bounded(lfmlib, oracle, gpu, capfd, monkeyp
     """A band5 hand-over forced to give up after one poll (LFM_UNPREDICT_SPIN=1)
     on a frame count that is not a multiple of 8: every band stops waiting
     once the status word carries the timeout, the device re-runs the frames
-    through band4, and the call returns exact pixels within a second,
+    through the one-wave kernel, and the call returns exact pixels within a second,
     reporting the timeout on stderr.  With LFM_UNPREDICT_FALLBACK=0 the same
     call fails instead of returning the pixels."""
     import time
@@ -592,6 +592,7 @@ def test_unpredict_forced_timeout_is_bounded(lfmlib, oracle, gpu, capfd, monkeyp
     with pytest.raises(lfmlib.LfmError):
         lfmlib.unpredict_device(d_sym, d_out, 520, 300, 4, 13, "tiles", 5)
     assert time.time() - t0 < 1.0
+    assert "not valid" in capfd.readouterr().err
     monkeypatch.delenv("LFM_UNPREDICT_SPIN")
     monkeypatch.delenv("LFM_UNPREDICT_FALLBACK")
     lfmlib.unpredict_device(d_sym, d_out, 520, 300, 4, 13, "tiles", 5)
@@ -942,7 +943,7 @@ def test_decode_chunk_pipeline(lfmlib, oracle, gpu, tmp_path, env):
 def test_unpredict_band_timeout_is_reported(lfmlib, oracle, gpu, tmp_path, fallback):
     """A band of the cross-CU inverse predictor (band5) that gives up waiting
     for the band above (here forced: one poll, LFM_UNPREDICT_SPIN=1) sets the
-    launch's error word: the launcher re-runs the frames through band4 and the
+    launch's error word: the device re-runs the frames (one-wave kernel) and the
     pixels are exact, or with LFM_UNPREDICT_FALLBACK=0 the read fails -- never
     wrong pixels returned as success."""
     import subprocess
