@@ -2235,6 +2235,21 @@ __device__ __forceinline__ uint64_t zero_byte_mask64(const uint32_t (&q)[kRle2Pe
     return Z;
 }
 
+// tile_out index swizzle: a thread writes its outputs at its own offset, and
+// the offsets of the 64 lanes lie one thread's output count apart -- often a
+// multiple of 32 words, i.e. one LDS bank.  XOR-ing the word index's low 5
+// bits with its 32-word row number spreads them over the banks; rows stay
+// whole, so the coalesced read-out (consecutive indices) is a permutation
+// inside each row, conflict-free as well.
+#ifndef LFM_RLE2_SWZ
+#define LFM_RLE2_SWZ 1
+#endif
+__device__ __forceinline__ uint32_t rle2_swz(uint32_t p)
+{
+    if constexpr (LFM_RLE2_SWZ) return p ^ (((p >> 6) & 31u) << 1);
+    else return p;
+}
+
 __global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4))) void rle2(Batch B)
 {
     constexpr uint32_t NW = kRle2Threads / 64;
@@ -2342,7 +2357,7 @@ __global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4)
             const uint32_t nb = (uint32_t)__popc(x & ((1u << d) - 1u));
             nrunB += nb;
             nrunA += d - nb;
-            for (uint32_t k = 0; k < d; ++k) tile_out[p + k] = (uint16_t)((x >> k) & 1u);
+            for (uint32_t k = 0; k < d; ++k) tile_out[rle2_swz(p + k)] = (uint16_t)((x >> k) & 1u);
         };
         // symbols v + 1: one write per value (zeros into a junk slot), the
         // position advanced past the digits of the run each one ends
@@ -2353,7 +2368,7 @@ __global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4)
                 const uint32_t v = (q[i >> 2] >> (8 * (i & 3))) & 0xFFu;
                 const bool nz = (NZ >> i) & 1u;
                 pos += nz && z ? run_digits(z) : 0u;
-                tile_out[nz ? pos : kRle2Tile + 64 + t] = (uint16_t)(v + 1u);
+                tile_out[rle2_swz(nz ? pos : kRle2Tile + 64 + t)] = (uint16_t)(v + 1u);
                 atomicAdd(&freq[nz && v > 4u ? v + 1u : kMaxAlpha + t], 1u);
                 hot += nz && v <= 4u ? 1ull << (16u * (v - 1u)) : 0ull;
                 pos += nz ? 1u : 0u;
@@ -2371,12 +2386,12 @@ __global__ __launch_bounds__(kRle2Threads) __attribute__((amdgpu_waves_per_eu(4)
         }
         if (has_last) {
             if (zend) digits(wr + w - 1u - dend, zend);
-            tile_out[wr + w - 1u] = (uint16_t)EOB;
+            tile_out[rle2_swz(wr + w - 1u)] = (uint16_t)EOB;
             atomicAdd(&freq[EOB], 1u);
         }
         __syncthreads();
         const uint32_t base = s_wr;
-        for (uint32_t i = t; i < tile_total; i += kRle2Threads) out[base + i] = tile_out[i];
+        for (uint32_t i = t; i < tile_total; i += kRle2Threads) out[base + i] = tile_out[rle2_swz(i)];
         __syncthreads();
         if (t == 0) {
             s_wr = base + tile_total;
