@@ -32,8 +32,6 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
-#include <type_traits>
-#include <utility>
 #include "lfm_cases.h"
 #include "lfm_hip.h"
 
@@ -1018,136 +1016,6 @@ __global__ __launch_bounds__(NCW * 64 + 64) void predict_vec(FrameSet p, int row
                                                       lane);
 }
 
-// ---------------------------------------------- register-window path (rw) --
-// Spatial frames, Nnum 13 / 15, W % 8 == 0.  No LDS and no barrier: every
-// wave is on its own.  A wave owns a strip of kRwOut = 496 output pixels of a
-// frame and walks down a piece of its rows (one wave per workgroup); lane l holds the 8 pixels
-// x0 = xs - 16 + 8 l .. x0 + 7 of a row, so lanes 0-1 carry the 16-pixel left
-// halo (T + 1 <= 16) and lanes 2-63 produce the strip.  The rows y - T - 1 ..
-// y + PD - 1 of the lane's 8 pixels sit in a ring of NR = T + 2 + PD
-// registers (uint32 x 4 each) indexed with compile-time slots (the row loop is
-// unrolled NR times), so each input pixel is read from HBM once and the next
-// PD rows are in flight while a row is computed (PD KiB per wave).  A row's
-// 24-pixel window [x0 - 16, x0 + 8) is its own 4 dwords plus the previous two
-// lanes' (two DPP wave_shr:1 shifts), which is exactly the Win24 the ring
-// kernel reads from LDS: the residual formulas (vec_fast_row /
-// vec_slow_row) are the same code.  The strips of a row piece run on one XCD
-// (launcher's block order); the halo pixels (the previous strip's last 16)
-// are read by both neighbours, from the same lines.
-constexpr int kRwOut = 496;
-
-template <class F, int... J>
-__device__ __forceinline__ void unroll_steps(F& f, std::integer_sequence<int, J...>)
-{
-    (f(std::integral_constant<int, J>{}), ...);
-}
-
-__device__ __forceinline__ uint32_t shr_lane(uint32_t v)  // lane l gets lane l - 1's v (lane 0: 0)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
-}
-
-__device__ __forceinline__ void rw_win(const v4u& x, Win24& r)
-{
-    const uint32_t b0 = shr_lane(x.x), b1 = shr_lane(x.y), b2 = shr_lane(x.z), b3 = shr_lane(x.w);
-    r.w[0] = shr_lane(b0); r.w[1] = shr_lane(b1); r.w[2] = shr_lane(b2); r.w[3] = shr_lane(b3);
-    r.w[4] = b0; r.w[5] = b1; r.w[6] = b2; r.w[7] = b3;
-    r.w[8] = x.x; r.w[9] = x.y; r.w[10] = x.z; r.w[11] = x.w;
-}
-
-template <int FAM, int K, int T, bool V0>
-__device__ __forceinline__ v4u rw_fast(const v4u& a0, const v4u& a1, const v4u& aT, const v4u& aT1, uint32_t u0bits,
-                                       const LaneMasks& lm, int x0)
-{
-    VecRows rw;
-    rw_win(a0, rw.r0);
-    rw_win(a1, rw.r1);
-    rw_win(aT, rw.rT);
-    rw_win(aT1, rw.rT1);
-    // FIRST: lanes of the frame's first lens column (x < T) take the TC_0Y
-    // formulas; in every other strip no lane has x0 < T and that per-lane
-    // branch is skipped as a whole
-    return vec_fast_row<FAM, K, T, false, V0, true>(rw, u0bits, lm, x0);
-}
-
-template <int FAM, int K, int T, int PD>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void predict_rw(FrameSet p, int rows_per_piece, int npiece, int xcd_map)
-{
-    constexpr int NR = T + 2 + PD;
-    const int lane = threadIdx.x;
-    const int nstrip = (p.W + kRwOut - 1) / kRwOut;
-    // one wave per workgroup; xcd_map: the strips of a row piece are blocks
-    // b, b + 8, ... (one XCD: the halo lines both neighbours read meet in one L2)
-    const int b = blockIdx.x;
-    int strip, group;
-    if (xcd_map) {
-        const int q = b >> 3;
-        strip = q % nstrip;
-        group = (q / nstrip) * 8 + (b & 7);
-    } else {
-        strip = b % nstrip;
-        group = b / nstrip;
-    }
-    const int piece = group % npiece, fz = group / npiece;
-    if (fz >= p.nz) return;
-    const int ys = piece * rows_per_piece, ye = min(ys + rows_per_piece, p.H);
-    if (ys >= ye) return;
-    const int W = p.W;
-    const size_t fs = (size_t)W * p.H;
-    const uint16_t* f = p.in + (size_t)fz * fs;
-    uint16_t* outf = p.out + (size_t)fz * fs;
-    const int xs = strip * kRwOut;
-    const int x0 = xs - 16 + 8 * lane;
-    const bool out_lane = lane >= 2 && x0 < W;
-    const uint16_t* fcol = f + min(max(x0, 0), W - 8);  // (clamped: halo lanes of strip 0, lanes past W)
-    auto ld = [&](int y) -> v4u {
-        const int yy = min(max(y, 0), ye - 1);
-        return *(const v4u*)(fcol + (size_t)yy * W);
-    };
-    // rows y < T (the frame's first lens row; piece 0 only): every case, per pixel
-    int y = ys;
-    for (; y < min(ye, T); ++y) {
-        VecRows rw;
-        rw_win(ld(y), rw.r0);
-        rw_win(ld(y - 1), rw.r1);
-        rw_win(ld(y - T), rw.rT);
-        rw_win(ld(y - T - 1), rw.rT1);
-        const v4u o = vec_slow_row<FAM, K, T, false>(rw, x0, y / T, y % T);
-        if (out_lane) __builtin_nontemporal_store(o, (v4u*)(outf + (size_t)y * W + x0));
-    }
-    if (y >= ye) return;
-    const int u0 = ((x0 % T) + T) % T;
-    uint32_t u0bits = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) u0bits |= (uint32_t)(((u0 + j) % T) == 0) << j;
-    const LaneMasks lm = lane_masks(u0bits, x0, T);
-    // ring slot of row r: (r - y + T + 1) mod NR; rows y - T - 1 .. y + PD - 1 primed
-    v4u ring[NR];
-#pragma unroll
-    for (int r = 0; r < NR - 1; ++r) ring[r] = ld(y - T - 1 + r);
-    int vy = y % T;
-    for (int g = y; g < ye; g += NR) {
-        // the NR steps of a round, unrolled by a fold over compile-time j (a
-        // loop the unroller declines would index the ring dynamically: scratch)
-        auto step = [&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            const int yr = g + j;
-            ring[(j + NR - 1) % NR] = ld(yr + PD);  // into row yr - T - 2's slot
-            if (yr < ye) {
-                const v4u& a0 = ring[(j + T + 1) % NR];
-                const v4u& a1 = ring[(j + T) % NR];
-                const v4u& aT = ring[(j + 1) % NR];
-                const v4u& aT1 = ring[j % NR];
-                const v4u o = vy == 0 ? rw_fast<FAM, K, T, true>(a0, a1, aT, aT1, u0bits, lm, x0)
-                                      : rw_fast<FAM, K, T, false>(a0, a1, aT, aT1, u0bits, lm, x0);
-                if (out_lane) __builtin_nontemporal_store(o, (v4u*)(outf + (size_t)yr * W + x0));
-                vy = vy + 1 == T ? 0 : vy + 1;
-            }
-        };
-        unroll_steps(step, std::make_integer_sequence<int, NR>{});
-    }
-}
-
 // ---- video volumes: frame pairs.  With the video bit, frame z is temporal
 // when z0 + z is odd and its residual needs the RAW previous frame z - 1,
 // which is the volume's own input: predict_vec reads it a second time (a
@@ -1463,53 +1331,12 @@ static hipError_t launch_vec_pairs(const FrameSet& p, hipStream_t st)
     return hipSuccess;
 }
 
-// register-window path: a ring of LFM_RW_NR rows (build time; 24 = 96 ring
-// VGPRs, the most that keeps every kernel at <= 128 VGPRs without spills, i.e.
-// 2 waves per SIMD), so PD = NR - T - 2 rows in flight per wave (7 for Nnum
-// 15, 9 for 13); pieces of rows so the waves fill the chip about 2.5 times
-// (LFM_PRED_RW_PIECES overrides; LFM_PRED_RW=0 keeps predict_vec)
-#ifndef LFM_RW_NR
-#define LFM_RW_NR 24
-#endif
-static bool rw_enabled()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("LFM_PRED_RW");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-}
-
-template <int FAM, int K, int T>
-static hipError_t launch_rw(const FrameSet& p, hipStream_t st)
-{
-    const int nstrip = (p.W + kRwOut - 1) / kRwOut;
-    static const int env_pieces = [] {
-        const char* e = std::getenv("LFM_PRED_RW_PIECES");
-        return e ? std::atoi(e) : 0;
-    }();
-    int npiece = env_pieces > 0 ? env_pieces : std::max(1, 2560 / std::max(1, p.nz * nstrip));
-    npiece = std::max(1, std::min(npiece, p.H / (2 * (p.T + 1))));
-    const int rows = (p.H + npiece - 1) / npiece;
-    npiece = (p.H + rows - 1) / rows;
-    const int ngroups = p.nz * npiece;
-    const int xcd_map = (ngroups % 8) == 0 && nstrip > 1;
-    hipLaunchKernelGGL((predict_rw<FAM, K, T, LFM_RW_NR - T - 2>), dim3(ngroups * nstrip), dim3(64), 0, st, p, rows,
-                       npiece, xcd_map);
-    return hipGetLastError();
-}
-
 template <int FAM, int K>
 static hipError_t launch_vec(const FrameSet& p, hipStream_t st)
 {
     using S = VecShape<FAM>;
     using PS = PairShape<FAM>;
     const bool pairs = p.video && p.nz >= 2;
-    // every frame spatial: the register-window kernel
-    if (rw_enabled() && !p.video && p.H >= 2 * (p.T + 1)) {
-        if (p.T == 15) return launch_rw<FAM, K, 15>(p, st);
-        return launch_rw<FAM, K, 13>(p, st);
-    }
     if (p.T == 15) {
         if (pairs) return launch_vec_pairs<FAM, K, 15, PS::WPR, PS::NCW, PS::RPW, PS::PD>(p, st);
         return launch_vec_shape<FAM, K, 15, S::WPR, S::NCW, S::RPW, S::PD>(p, st);

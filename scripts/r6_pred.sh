@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${1:-r6pred}; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "register_window or golden_predictor or fast_kernel or video_frame_pairs or candidates or z0_offset" > $O/pytest_pred.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "spatial_stack or golden_predictor or fast_kernel or video_frame_pairs or candidates or z0_offset" > $O/pytest_pred.log 2>&1; rc=$?
 tail -n 3 $O/pytest_pred.log
 [ $rc -ne 0 ] && exit $rc
 for r in 1 2; do

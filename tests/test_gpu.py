@@ -82,13 +82,12 @@ def test_fast_kernel_vs_oracle(lfmlib, oracle, gpu, W, H, T):
 
 @pytest.mark.parametrize("W,H,T,Z", [(2048, 300, 15, 3), (496, 64, 13, 2), (504, 100, 15, 2), (992, 250, 13, 3),
                                       (1000, 34, 15, 1), (520, 700, 13, 1), (32, 40, 15, 2), (4096, 64, 13, 1)])
-def test_register_window_kernel_vs_oracle(lfmlib, oracle, gpu, W, H, T, Z):
-    """Spatial stacks (no video bit) take predict_rw: 496-pixel strips whose
-    lanes 0-1 hold the left halo, a register ring of rows walked down row
-    pieces.  Widths at and around the strip seams (one strip, a partial last
-    strip, many strips), heights from one lens row plus one to many pieces
-    (the ring's round tails), every family and predictor, one full-range
-    frame for the int16 wrap."""
+def test_spatial_stack_shapes_vs_oracle(lfmlib, oracle, gpu, W, H, T, Z):
+    """Spatial stacks (no video bit, predict_vec): widths at and around strip
+    seams (one strip, a partial last strip, many strips), heights from one
+    lens row plus one to many row pieces, every family and predictor, one
+    full-range frame for the int16 wrap.  (Written for the round-6
+    register-window kernel, which was exact but slower and was dropped.)"""
     torch = gpu
     stack = oracle.synthetic_lf(W, H, Z=Z, T=T, seed=W * 3 + H + Z)[0, 0]
     stack[-1] = np.random.default_rng(W + H).integers(0, 65536, size=(H, W), dtype=np.uint16)
