@@ -3734,7 +3734,10 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         hipLaunchKernelGGL(huff_select_reg, dim3(count), dim3(kHuffThreads), 0, st, B);
         // uniform heaps, 32 per workgroup: u32 entries for the narrow tables,
         // u64 for the streams rle2 listed, in one launch
-        constexpr uint32_t kPlane = 32;
+#ifndef LFM_HUFF_PLANE
+#define LFM_HUFF_PLANE 32
+#endif
+        constexpr uint32_t kPlane = LFM_HUFF_PLANE;  // (stream, table) heaps per wave
         const uint32_t nn = (count * kMaxGroups + kPlane - 1) / kPlane;
         const uint32_t nw = (nwide * kMaxGroups + kPlane / 2 - 1) / (kPlane / 2);
         hipLaunchKernelGGL(huff_lengths_heap<kPlane>, dim3(nn + nw), dim3(64), 0, st, B, nw, nwide);

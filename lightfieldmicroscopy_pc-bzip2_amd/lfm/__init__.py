@@ -89,7 +89,9 @@ def lib():
     L.readKLBstackInPlace.argtypes = [ctypes.c_char_p, vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.readKLBroiInPlace.argtypes = [ctypes.c_char_p, vp, u32p, u32p, ctypes.c_int]
     L.lfm_version.restype = ctypes.c_char_p
-    if L.lfm_api_version() != 2:  # lfm_decode_memory_roi's argument list (lfm_api.h)
+    # lfm_decode_memory_roi's argument list (lfm_api.h); a library without the
+    # version symbol is a round-5 build, whose list is the same
+    if hasattr(L, "lfm_api_version") and L.lfm_api_version() != 2:
         raise OSError("liblfm.so API version %d, this binding needs 2" % L.lfm_api_version())
     L.writeLFMstack_c.argtypes = [vp, ctypes.c_char_p, u32p, ctypes.c_int, ctypes.c_int, f32p, u32p, ctypes.c_int,
                                   ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
