@@ -2245,6 +2245,15 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     };
     std::vector<uint8_t> hb(block_bytes);
     int rc = 0;
+    const double t_hb = ms(t_start, clk::now());
+    // LFM_DECODE_TIMING: a timeline of the pipeline's steps (ms since start)
+    std::mutex tlmu;
+    std::vector<std::pair<std::string, double>> tl;
+    auto mark = [&](const char* what, uint64_t c) {
+        if (!timing) return;
+        std::lock_guard<std::mutex> lk(tlmu);
+        tl.emplace_back(std::string(what) + " " + std::to_string(c), ms(t_start, clk::now()));
+    };
     // The image comes down into the caller's buffer, usually fresh pages (a
     // new numpy array, readKLBstack's malloc): the download's host copies used
     // to take a first-touch fault per 4 KiB page (config 3: 131 072 faults,
@@ -2268,13 +2277,23 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             });
         });
     }
-    if (hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, DB.st[0]) != hipSuccess ||
-        hipStreamSynchronize(DB.st[0]) != hipSuccess)
-        rc = 3;
+    mark("prefault-started", 0);
+    // the 64 zero bytes past the payload (the bit window's lookahead of the
+    // last stream): LFM_DECODE_SLACK=1 queues them on the last chunk's stream
+    // (stream order puts them before its kernels), 0 synchronises here
+    static const int slack_mode = env_int("LFM_DECODE_SLACK", 1);
+    {
+        hipStream_t sst = slack_mode ? DB.st[(nch - 1) % nslot] : DB.st[0];
+        if (hipMemsetAsync((uint8_t*)d_pay + offs[nb], 0, 64, sst) != hipSuccess) rc = 3;
+        mark("memset-issued", 0);
+        if (!slack_mode && hipStreamSynchronize(sst) != hipSuccess) rc = 3;
+    }
+    mark("memset", 0);
     // per chunk: its scatter + inverse predictor done (the download waits for it)
     std::vector<hipEvent_t> cev(nch, nullptr);
     for (uint64_t c = 0; c < nch && !rc; ++c)
         if (hipEventCreateWithFlags(&cev[c], hipEventDisableTiming) != hipSuccess) rc = 3;
+    mark("events", 0);
     // host side of chunk c once its streams are decoded: host-library blocks,
     // then scatter and inverse predictor queued behind them (no wait)
     auto finish = [&](uint64_t c) -> int {
@@ -2355,6 +2374,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                 if (dl_ready <= c) return;  // stopped
             }
             auto t0 = clk::now();
+            mark("dl-start", c);
             uint64_t f0, f1;
             frames(c, f0, f1);
             const size_t o0 = f0 * frame_bytes, n = (f1 - f0) * frame_bytes;
@@ -2364,6 +2384,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                 drc = 3;
                 return;
             }
+            mark("dl-ready", c);
             // the chunk's inverse predictor launches: a hand-over that timed
             // out and was not repaired on the device fails the read
             if (predicted)
@@ -2379,6 +2400,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                 return;
             }
             t_down += ms(t0, clk::now());
+            mark("dl-end", c);
         }
     });
     auto hand_over = [&](uint64_t c) {
@@ -2388,6 +2410,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
         }
         dcv.notify_all();
     };
+    mark("downloader-started", 0);
     for (uint64_t c = 0; c < nch && !rc; ++c) {
         const int q = (int)(c % nslot);
         const uint64_t b0 = c * batch, cnt = std::min<uint64_t>(batch, nb - b0);
@@ -2397,18 +2420,21 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             break;
         }
         t_up += ms(t0, clk::now());
-        if (timing) std::fprintf(stderr, "decode: chunk %llu upload %.2f ms\n", (unsigned long long)c, ms(t0, clk::now()));
+        mark("uploaded", c);
         if (lfm_hip_bunzip2_issue(d_pay, offs.data() + b0, (uint32_t)cnt, d_blk[q], block_bytes, d_ws[q], ws, hs[q],
                                   hs[q] + batch, DB.st[q]) != LFM_HIP_OK) {
             rc = 3;
             break;
         }
+        mark("issued", c);
         if (c > 0) {
             rc = finish(c - 1);
+            mark("finished", c - 1);
             if (!rc) hand_over(c - 1);
         }
     }
     if (!rc) rc = finish(nch - 1);
+    mark("finished", nch - 1);
     if (!rc) hand_over(nch - 1);
     {
         std::lock_guard<std::mutex> lk(dmu);
@@ -2416,11 +2442,18 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     }
     dcv.notify_all();
     downloader.join();
+    mark("joined", nch);
     if (prefault.joinable()) prefault.join();  // (not reached: the downloader joins it first)
     if (!rc) rc = drc;
     for (int q = 0; q < nslot; ++q) (void)hipStreamSynchronize(DB.st[q]);  // nothing may still run on the buffers
     for (hipEvent_t e : cev)
         if (e) (void)hipEventDestroy(e);
+    if (timing) {
+        std::string line = "decode timeline: alloc@" + std::to_string(ms(t_start, t_alloc)).substr(0, 6) +
+                           " hb@" + std::to_string(t_hb).substr(0, 6);
+        for (auto& e : tl) line += " " + e.first + "@" + std::to_string(e.second).substr(0, 6);
+        std::fprintf(stderr, "%s\n", line.c_str());
+    }
     if (timing)
         std::fprintf(stderr,
                      "decode: %llu chunks of <= %llu blocks, alloc %.2f ms, upload %.2f, wait %.2f, host + kernels "

@@ -22,6 +22,8 @@ k, _ = lfm.select_device(d[0], X, Y, T, "angle")
 enc = lfm.Encoder(device=0, num_threads=16)  # owns the .lfm buffer (copy=False)
 buf, _ = enc.encode_slab(d, 0, header_version=forced_request(k), nnum=T, copy=False)
 buf = bytes(buf)
+if os.environ.get("CLOSE_ENC", "0") != "0":  # a reader process has no encoder (bench.py closes it too)
+    enc.close()
 ref = d.cpu().numpy().view(np.uint16)
 for it in range(3):
     img = None  # free the previous result first (its unmap is not the decode's)
