@@ -503,6 +503,7 @@ void Encoder::Inflight::release()
     {
         std::lock_guard<std::mutex> lk(mu);
         released = true;
+        mtf_done = true;
     }
     cv.notify_all();
 }
@@ -512,9 +513,25 @@ void Encoder::Inflight::reach()
     {
         std::lock_guard<std::mutex> lk(mu);
         ++reached;
-        if (need > 0 && reached >= need) released = true;
+        if (need > 0 && reached >= need) released = mtf_done = true;
     }
     cv.notify_all();
+}
+
+void Encoder::Inflight::reach2()
+{
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        ++reached2;
+        if (need > 0 && reached2 >= need) mtf_done = true;
+    }
+    cv.notify_all();
+}
+
+void Encoder::Inflight::wait_mtf()
+{
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return mtf_done || released; });
 }
 
 void Encoder::Inflight::wait_release()
@@ -562,8 +579,10 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
     {
         std::lock_guard<std::mutex> lk(f.mu);
         f.reached = 0;
+        f.reached2 = 0;
         f.need = 0;
         f.released = false;
+        f.mtf_done = false;
     }
     if (ticket) *ticket = f.ticket;
     par_ ^= 1;
@@ -573,6 +592,11 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
         f.release();
         return rc;
     };
+    // LFM_SELECT_AT=2: a device stack's selection and predictor stage wait
+    // until the previous encode is past its MTF stage, i.e. in its
+    // latency-bound Huffman rounds, instead of sharing the CUs with its sorts
+    static const int select_at = env_int("LFM_SELECT_AT", 0);
+    if (select_at == 2 && dev && host_early) fly_[p ^ 1].wait_mtf();
     if (pre && host_early)
         if (int rc = select_now()) return fail(rc);
     if (pre_k >= 0) {
@@ -1323,6 +1347,7 @@ int Encoder::gpu_compress(const uint8_t* d_sym, klb_image_header& h, Sink& sink,
                 lfm_hip_bzip2_set_stage_hook(
                     [](void* c, int stage) {
                         auto* r = (ReachOnce*)c;
+                        if (stage == 2) r->f->reach2();
                         if (stage == 3 && !r->done) {
                             r->done = true;
                             r->f->reach();

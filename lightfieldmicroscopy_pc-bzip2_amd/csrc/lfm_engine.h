@@ -180,9 +180,13 @@ private:
         int reached = 0;      // batches of the last round past the release stage
         int need = 0;         // ... needed to release the next submit (0: not yet known)
         bool released = true;
+        int reached2 = 0;     // batches of the last round past the MTF stage (stage 2)
+        bool mtf_done = true; // every last-round batch is past stage 2 (or released)
         void release();
         void wait_release();
         void reach();         // one last-round batch passed the release stage
+        void reach2();        // one last-round batch passed its MTF stage
+        void wait_mtf();
     };
     // Host stacks for the GPU bzip2 path go up in chunks of whole frames on
     // up_stream_ (one uploader thread per encode), each chunk predicted on
