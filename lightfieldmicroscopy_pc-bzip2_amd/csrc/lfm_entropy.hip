@@ -229,7 +229,10 @@ __global__ __launch_bounds__(256) void ent_link(Jobs J, uint8_t* __restrict__ pa
 // quarters of a job are blocks b, b + 8, b + 16, b + 24 (one XCD: the job's
 // bytes are read from one L2).  Bin 0 -- (0, 0), the high bytes of small
 // symbols -- is counted in registers.
-constexpr int kRowThreads = 512;
+#ifndef LFM_ENT_ROW_THREADS
+#define LFM_ENT_ROW_THREADS 512
+#endif
+constexpr int kRowThreads = LFM_ENT_ROW_THREADS;
 __global__ __launch_bounds__(kRowThreads) void ent_rows(Jobs J, const uint8_t* __restrict__ part,
                                                         const uint32_t* __restrict__ meta, float* __restrict__ rows)
 {
