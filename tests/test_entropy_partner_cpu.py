@@ -52,7 +52,7 @@ def hist_by_partner(c):
 
 @pytest.mark.parametrize("kind", ["skewed", "uniform", "two_bytes", "zeros", "no_zero", "runs"])
 def test_partner_histogram_equals_sorted_pairs(kind):
-    rng = np.random.default_rng(hash(kind) % (1 << 32))
+    rng = np.random.default_rng(sum(map(ord, kind)))  # (fixed per case)
     for S in (1, 2, 3, 17, 64, 65, 200, 999):
         if kind == "skewed":
             c = np.minimum(np.abs(rng.normal(0, 6, S)).astype(np.int64), 255)
