@@ -1069,6 +1069,46 @@ __global__ __launch_bounds__(256) void tie_runs_direct(Batch B, const uint32_t* 
     }
 }
 
+// Thread t's items of chunk [cb, cb + m), striped (item q is slot q * TH + t:
+// coalesced): the values and their 8-byte keys rebuilt from the text; items
+// past m get key ~0, value 0.  Every load is unconditional (clamped
+// indices) and all of one kind are issued before any is used: one memory
+// round trip for the values and one for the text of all IPT items (under
+// per-item branches the compiler waited for each item's loads in turn: 2 IPT
+// round trips).
+template <int TH, int IPT>
+__device__ __forceinline__ void chunk_load(const Batch& B, uint32_t cb, uint32_t m, uint32_t t, uint64_t (&k)[IPT],
+                                           uint32_t (&v)[IPT])
+{
+    const uint32_t s = cb / B.cap, n = B.n[s];
+    const uint8_t* T = B.T + (size_t)s * B.cap;
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) v[q] = B.vals_a[cb + min(q * TH + t, m ? m - 1u : 0u)];
+    uint32_t d[IPT][3];
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t i = v[q] & kIdxMask;
+        const uint32_t* w = (const uint32_t*)(T + ((i + 8u <= n ? i : 0u) & ~3u));
+        d[q][0] = w[0];
+        d[q][1] = w[1];
+        d[q][2] = w[2];
+    }
+#pragma unroll
+    for (int q = 0; q < IPT; ++q) {
+        const uint32_t j = q * TH + t, i = v[q] & kIdxMask;
+        if (j >= m) {
+            k[q] = ~0ull;
+            v[q] = 0u;
+        } else if (i + 8u <= n) {  // rot_key8_fast's fast path on the loaded dwords
+            const uint32_t sh = (i & 3u) * 8u;
+            const uint64_t x = (uint64_t)d[q][0] | ((uint64_t)d[q][1] << 32);
+            k[q] = __builtin_bswap64(sh ? (x >> sh) | ((uint64_t)d[q][2] << (64u - sh)) : x);
+        } else {
+            k[q] = rot_key8_fast(T, n, i);
+        }
+    }
+}
+
 // The chunk's keys / values are loaded striped (element q * TH + t: coalesced),
 // sorted (rocPRIM block merge sort: thread t ends with sorted positions
 // t * IPT .. t * IPT + IPT - 1), the still-tied flags come from the
@@ -1101,39 +1141,9 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
         Xch x;
     } sm;
     const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
-    const uint32_t s = cb / B.cap, n = B.n[s];
-    const uint8_t* T = B.T + (size_t)s * B.cap;
     uint64_t k[IPT];
     uint32_t v[IPT];
-    // every load unconditional (clamped indices), all of one kind issued
-    // before any is used: one memory round trip for the values and one for
-    // the text of all IPT items (under per-item branches the compiler waited
-    // for each item's loads in turn: 2 IPT round trips)
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) v[q] = B.vals_a[cb + min(q * TH + t, m ? m - 1u : 0u)];
-    uint32_t d[IPT][3];
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const uint32_t i = v[q] & kIdxMask;
-        const uint32_t* w = (const uint32_t*)(T + ((i + 8u <= n ? i : 0u) & ~3u));
-        d[q][0] = w[0];
-        d[q][1] = w[1];
-        d[q][2] = w[2];
-    }
-#pragma unroll
-    for (int q = 0; q < IPT; ++q) {
-        const uint32_t j = q * TH + t, i = v[q] & kIdxMask;
-        if (j >= m) {
-            k[q] = ~0ull;
-            v[q] = 0u;
-        } else if (i + 8u <= n) {  // rot_key8_fast's fast path on the loaded dwords
-            const uint32_t sh = (i & 3u) * 8u;
-            const uint64_t x = (uint64_t)d[q][0] | ((uint64_t)d[q][1] << 32);
-            k[q] = __builtin_bswap64(sh ? (x >> sh) | ((uint64_t)d[q][2] << (64u - sh)) : x);
-        } else {
-            k[q] = rot_key8_fast(T, n, i);
-        }
-    }
+    chunk_load<TH, IPT>(B, cb, m, t, k, v);
     // the sort's valid-item count refers to the blocked arrangement
     ExK().striped_to_blocked(k, k, sm.ek);
     __syncthreads();
@@ -1172,6 +1182,149 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     if (__any(nt)) {
         for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
         if ((threadIdx.x & 63) == 0 && nt) atomicAdd(&B.done[cb / B.cap], nt);
+    }
+}
+
+// bwt_chunk_rsort: bwt_chunk_sort's contract (a chunk's rotations ordered by
+// their 8-byte big-endian prefix into sa, the still-tied flags into uflag and
+// B.done) as a hand-written LDS radix sort, least significant digit first,
+// over only the key bits that vary inside the chunk: D = OR(k) & ~AND(k) over
+// its keys, and each pass takes the 8-bit digit at s, the next one at the
+// lowest varying bit >= s + 8.  Bits constant across the chunk -- the
+// bucket's leading bits, the zero high bits of small symbols' bytes -- cost no
+// pass.  Ranking: a wave finds the lanes sharing an item's digit with 8
+// ballots, keeps a running count per (digit, wave) in LDS, and one exclusive
+// scan over the digit-major (digit, wave) counts gives every digit's start.
+// Positions are ordered by wave, then item, then lane, so each pass is stable
+// as LSD needs.  The order of equal keys is free (tie_runs_direct and the tie
+// rounds order them), so the first pass ranks the items as loaded.
+template <int TH, int IPT>
+__global__ __launch_bounds__(TH) void bwt_chunk_rsort(Batch B, const uint32_t* __restrict__ cbp,
+                                                      const uint32_t* __restrict__ cep, uint32_t nch, uint32_t per)
+{
+    const uint32_t c = per ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;  // (XCD order, as bwt_chunk_sort)
+    if (c >= nch) return;
+    constexpr uint32_t NW = TH / 64, NI = TH * IPT, WI = 64 * IPT;
+    static_assert(256 * NW == 4 * TH, "four (digit, wave) counters per thread");
+    __shared__ uint64_t sk[NI];
+    __shared__ uint32_t sv[NI];
+    __shared__ uint32_t hist[256 * NW];  // [digit][wave]
+    __shared__ uint32_t wsum[NW];
+    __shared__ uint64_t wor[NW], wand[NW];
+    const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint64_t k[IPT];
+    uint32_t v[IPT];
+    chunk_load<TH, IPT>(B, cb, m, t, k, v);
+    {  // the varying bits
+        uint64_t o = 0, a = ~0ull;
+#pragma unroll
+        for (int q = 0; q < IPT; ++q)
+            if (q * TH + t < m) {
+                o |= k[q];
+                a &= k[q];
+            }
+        for (int d = 32; d > 0; d >>= 1) {
+            o |= __shfl_xor(o, d);
+            a &= __shfl_xor(a, d);
+        }
+        if (lane == 0) {
+            wor[w] = o;
+            wand[w] = a;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hist[4 * t + e] = 0;
+    }
+    __syncthreads();
+    uint64_t D = 0, A = ~0ull;
+#pragma unroll
+    for (uint32_t x = 0; x < NW; ++x) {
+        D |= wor[x];
+        A &= wand[x];
+    }
+    D &= ~A;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    bool first = true;
+    for (uint32_t s = D ? (uint32_t)__builtin_ctzll(D) : 64u; s < 64u;) {
+        uint32_t r[IPT], dg[IPT];
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            const bool ok = first ? q * TH + t < m : w * WI + q * 64 + lane < m;
+            const uint32_t d = (uint32_t)(k[q] >> s) & 0xFFu;
+            uint64_t same = __ballot(ok);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {  // keep the lanes whose bit b equals this lane's
+                const int32_t e = (int32_t)(d << (31 - b)) >> 31;  // 0 / -1
+                const uint64_t bb = __ballot(e != 0);
+                same &= ~(bb ^ (uint64_t)(int64_t)e);
+            }
+            const uint32_t below = __popcll(same & lt);
+            uint32_t* h = &hist[d * NW + w];
+            const uint32_t base = ok ? *h : 0u;
+            if (ok && below == 0) *h = base + __popcll(same);
+            r[q] = ok ? base + below : ~0u;
+            dg[q] = d;
+        }
+        __syncthreads();
+        {  // exclusive scan of the counts, digit-major
+            const uint32_t x0 = hist[4 * t], x1 = hist[4 * t + 1], x2 = hist[4 * t + 2], x3 = hist[4 * t + 3];
+            const uint32_t sum = x0 + x1 + x2 + x3;
+            uint32_t inc = sum;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(inc, d);
+                if ((int)lane >= d) inc += y;
+            }
+            if (lane == 63) wsum[w] = inc;
+            __syncthreads();
+            uint32_t p = inc - sum;
+            for (uint32_t x = 0; x < w; ++x) p += wsum[x];
+            hist[4 * t] = p;
+            hist[4 * t + 1] = p + x0;
+            hist[4 * t + 2] = p + x0 + x1;
+            hist[4 * t + 3] = p + x0 + x1 + x2;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < IPT; ++q)
+            if (r[q] != ~0u) {
+                const uint32_t to = hist[dg[q] * NW + w] + r[q];
+                sk[to] = k[q];
+                sv[to] = v[q];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < IPT; ++q) {
+            const uint32_t p = w * WI + q * 64 + lane;
+            k[q] = sk[p];
+            v[q] = sv[p];
+        }
+        // this wave's counters back to zero (every wave has read its
+        // digits' starts before the barrier; only this wave counts into them)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hist[(lane + 64 * e) * NW + w] = 0;
+        first = false;
+        const uint64_t rest = s + 8u < 64u ? D >> (s + 8u) : 0ull;
+        s = rest ? s + 8u + (uint32_t)__builtin_ctzll(rest) : 64u;
+    }
+    if (first) {  // every key equal: no pass ran, the items as loaded
+#pragma unroll
+        for (int q = 0; q < IPT; ++q)
+            if (q * TH + t < m) {
+                sk[q * TH + t] = k[q];
+                sv[q * TH + t] = v[q];
+            }
+        __syncthreads();
+    }
+    uint32_t nt = 0;
+    for (uint32_t j = t; j < m; j += TH) {
+        const uint64_t kj = sk[j];
+        const bool f = (j > 0 && sk[j - 1] == kj) || (j + 1 < m && sk[j + 1] == kj);
+        B.sa[cb + j] = sv[j];
+        B.uflag[cb + j] = f ? 1 : 0;
+        nt += f ? 1u : 0u;
+    }
+    if (__any(nt)) {
+        for (int d = 32; d > 0; d >>= 1) nt += __shfl_xor(nt, d);
+        if (lane == 0 && nt) atomicAdd(&B.done[cb / B.cap], nt);
     }
 }
 
@@ -3519,6 +3672,14 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
 #ifndef LFM_BWT_FORCE_FULL
 #define LFM_BWT_FORCE_FULL 0  // timing variants: every rotation sorted, no induction
 #endif
+#ifndef LFM_BWT_RSORT
+#define LFM_BWT_RSORT 0  // 1: the hand-written radix chunk sort (bwt_chunk_rsort) instead of rocPRIM's merge sort
+#endif
+#if LFM_BWT_RSORT
+#define LFM_CHUNK_SORT bwt_chunk_rsort
+#else
+#define LFM_CHUNK_SORT bwt_chunk_sort
+#endif
     for (B.it_full = LFM_BWT_FORCE_FULL;; B.it_full = 1) {
         ChunkLists CL;
         const size_t q = N / 4;  // chunk lists in the cl0 / cl1 areas (at most 3 n / kChunk + 1 chunks per stream)
@@ -3544,17 +3705,17 @@ extern "C" int lfm_hip_bzip2_blocks(const void* d_img, const uint32_t dims[5], c
         uint32_t per = 0;
         if (nch[5]) {
             const dim3 g = cs_grid(nch[5], per);
-            hipLaunchKernelGGL((bwt_chunk_sort<kTinyCap / kCsItems, kCsItems>), g, dim3(kTinyCap / kCsItems), 0, st, B,
+            hipLaunchKernelGGL((LFM_CHUNK_SORT<kTinyCap / kCsItems, kCsItems>), g, dim3(kTinyCap / kCsItems), 0, st, B,
                                CL.b[3], CL.e[3], nch[5], per);
         }
         if (nch[0]) {
             const dim3 g = cs_grid(nch[0], per);
-            hipLaunchKernelGGL((bwt_chunk_sort<kCsThreads, kCsItems>), g, dim3(kCsThreads), 0, st, B, CL.b[0], CL.e[0],
+            hipLaunchKernelGGL((LFM_CHUNK_SORT<kCsThreads, kCsItems>), g, dim3(kCsThreads), 0, st, B, CL.b[0], CL.e[0],
                                nch[0], per);
         }
         if (nch[1]) {
             const dim3 g = cs_grid(nch[1], per);
-            hipLaunchKernelGGL((bwt_chunk_sort<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
+            hipLaunchKernelGGL((LFM_CHUNK_SORT<kBigThreads, kBigItems>), g, dim3(kBigThreads), 0, st, B, CL.b[1],
                                CL.e[1], nch[1], per);
         }
         if (nch[2]) {

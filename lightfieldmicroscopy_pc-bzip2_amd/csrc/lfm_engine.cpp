@@ -2285,10 +2285,10 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     // download 11-24 ms for 537 MB).  While the GPU decodes, a helper thread
     // asks for huge pages and touches one byte per page of the destination, so
     // the downloads copy into mapped memory (LFM_DECODE_PREFAULT=0: off).
-    static const bool prefault_on = env_int("LFM_DECODE_PREFAULT", 1) != 0;
+    static const int prefault_mode = env_int("LFM_DECODE_PREFAULT", 1);  // 2: started after the first upload
     std::thread prefault;  // joined by the downloader before its first copy
-    if (prefault_on) {
-        prefault = std::thread([img, img_bytes, threads]() {
+    auto start_prefault = [&]() {
+        prefault = std::thread([img, img_bytes, threads, &mark]() {
             const size_t pg = (size_t)sysconf(_SC_PAGESIZE), huge = (size_t)2 << 20;
             const uintptr_t a0 = ((uintptr_t)img + huge - 1) & ~(uintptr_t)(huge - 1);
             const uintptr_t a1 = ((uintptr_t)img + img_bytes) & ~(uintptr_t)(huge - 1);
@@ -2300,9 +2300,11 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                 const size_t e = std::min(img_bytes, (size_t)(i + 1) * piece);
                 for (size_t o = (size_t)i * piece; o < e; o += pg) q[o] = 0;
             });
+            mark("prefault-done", 0);
         });
-    }
-    mark("prefault-started", 0);
+        mark("prefault-started", 0);
+    };
+    if (prefault_mode == 1) start_prefault();
     // the 64 zero bytes past the payload (the bit window's lookahead of the
     // last stream): LFM_DECODE_SLACK=1 queues them on the last chunk's stream
     // (stream order puts them before its kernels), 0 synchronises here
@@ -2391,13 +2393,14 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     (void)hipGetDevice(&dev);
     std::thread downloader([&]() {
         (void)hipSetDevice(dev);
-        if (prefault.joinable()) prefault.join();  // (done long before the first chunk is decoded)
         for (uint64_t c = 0; c < nch; ++c) {
             {
                 std::unique_lock<std::mutex> lk(dmu);
                 dcv.wait(lk, [&] { return dl_ready > c || dl_stop; });
                 if (dl_ready <= c) return;  // stopped
             }
+            // (started before chunk 0 was handed over; done long before it is decoded)
+            if (c == 0 && prefault.joinable()) prefault.join();
             auto t0 = clk::now();
             mark("dl-start", c);
             uint64_t f0, f1;
@@ -2446,6 +2449,7 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
         }
         t_up += ms(t0, clk::now());
         mark("uploaded", c);
+        if (c == 0 && prefault_mode == 2) start_prefault();
         if (lfm_hip_bunzip2_issue(d_pay, offs.data() + b0, (uint32_t)cnt, d_blk[q], block_bytes, d_ws[q], ws, hs[q],
                                   hs[q] + batch, DB.st[q]) != LFM_HIP_OK) {
             rc = 3;

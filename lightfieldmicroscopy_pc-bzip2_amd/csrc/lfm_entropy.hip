@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void ent_link(Jobs J, uint8_t* __restrict__ pa
 // bytes are read from one L2).  Bin 0 -- (0, 0), the high bytes of small
 // symbols -- is counted in registers.
 #ifndef LFM_ENT_ROW_THREADS
-#define LFM_ENT_ROW_THREADS 512
+#define LFM_ENT_ROW_THREADS 1024  // (512: a config-3 selection 0.51 ms, 1 024: 0.50; profiles/r06_ab_select_ent_rows.txt)
 #endif
 constexpr int kRowThreads = LFM_ENT_ROW_THREADS;
 __global__ __launch_bounds__(kRowThreads) void ent_rows(Jobs J, const uint8_t* __restrict__ part,
