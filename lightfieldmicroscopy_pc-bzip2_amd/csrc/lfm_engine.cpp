@@ -1915,6 +1915,14 @@ bool staged_h2d(void* d_dst, const void* h_src, size_t n, hipStream_t st, int th
 // the CUs.  Returns false if HSA cannot take the copy (nothing was issued on
 // a false return before the first chunk; the caller falls back).  The
 // destination stream must be idle (the caller synchronises it).
+// the wait state of the staged SDMA copies' signal waits (LFM_SDMA_WAIT: 0
+// blocked, the default; 1 active)
+hsa_wait_state_t sdma_wait_state()
+{
+    static const int m = env_int("LFM_SDMA_WAIT", 0);
+    return m == 1 ? HSA_WAIT_STATE_ACTIVE : HSA_WAIT_STATE_BLOCKED;
+}
+
 bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
 {
     const hsa_agent_t* cpu = hsa_cpu_agent();
@@ -1934,18 +1942,20 @@ bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
     }
     bool ok = true;
     static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
-    double t_wait = 0, t_copy = 0;
+    double t_wait = 0, t_copy = 0, t_first = 0;
     auto now = [] { return std::chrono::steady_clock::now(); };
     for (size_t off = 0, i = 0; ok && off < n; off += Staging::kChunk, ++i) {
         const int b = (int)(i & 1);
         const size_t len = std::min(Staging::kChunk, n - off);
         auto t0 = now();
         if (i >= 2) ok = hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX,
-                                                   HSA_WAIT_STATE_BLOCKED) == 0;
+                                                   sdma_wait_state()) == 0;
         if (!ok) break;
         auto t1 = now();
         par_memcpy_impl(S.buf[b], (const uint8_t*)h_src + off, len, threads);
-        t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        const double w = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        t_wait += w;
+        if (i == 2) t_first = w;
         t_copy += std::chrono::duration<double, std::milli>(now() - t1).count();
         hsa_signal_store_relaxed(sig[b], 1);
         ok = hsa_amd_memory_async_copy((uint8_t*)d_dst + off, info.agentOwner, S.buf[b], *cpu, len, 0, nullptr,
@@ -1954,11 +1964,13 @@ bool sdma_staged_h2d(void* d_dst, const void* h_src, size_t n, int threads)
     }
     auto t_tail = now();
     for (int b = 0; b < 2; ++b)
-        if (hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) != 0)
+        if (hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, sdma_wait_state()) != 0)
             ok = false;
     if (timing)
-        std::fprintf(stderr, "sdma h2d: %zu bytes, host copies %.2f ms, waits %.2f ms, last copy %.2f ms, %d threads\n",
-                     n, t_copy, t_wait, std::chrono::duration<double, std::milli>(now() - t_tail).count(), threads);
+        std::fprintf(stderr,
+                     "sdma h2d: %zu bytes, host copies %.2f ms, waits %.2f ms (first %.2f), last copy %.2f ms, %d threads\n",
+                     n, t_copy, t_wait, t_first, std::chrono::duration<double, std::milli>(now() - t_tail).count(),
+                     threads);
     hsa_signal_destroy(sig[0]);
     hsa_signal_destroy(sig[1]);
     S.used[0] = S.used[1] = false;  // the chunks are free (no HIP event pending on them)
@@ -2000,7 +2012,7 @@ bool sdma_staged_d2h(void* h_dst, const void* d_src, size_t n, int threads, Stag
         return true;
     };
     auto wait = [&](int b) {
-        return hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) == 0;
+        return hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, sdma_wait_state()) == 0;
     };
     bool ok = issue(0);
     for (size_t i = 0; ok && i < nc; ++i) {
@@ -2285,6 +2297,13 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
     // download 11-24 ms for 537 MB).  While the GPU decodes, a helper thread
     // asks for huge pages and touches one byte per page of the destination, so
     // the downloads copy into mapped memory (LFM_DECODE_PREFAULT=0: off).
+    // LFM_DECODE_DMA_PROBE=1 (diagnosis): a 64 KiB staged SDMA upload, timed,
+    // before the decode's own steps start
+    if (env_int("LFM_DECODE_DMA_PROBE", 0) == 1 && offs[nb] >= 65536) {
+        const auto p0 = clk::now();
+        const bool pok = sdma_staged_h2d(d_pay, payload, 65536, 1);
+        std::fprintf(stderr, "dma probe: 64 KiB upload %.3f ms (%s)\n", ms(p0, clk::now()), pok ? "ok" : "failed");
+    }
     static const int prefault_mode = env_int("LFM_DECODE_PREFAULT", 1);  // 2: started after the first upload
     std::thread prefault;  // joined by the downloader before its first copy
     auto start_prefault = [&]() {
