@@ -577,6 +577,9 @@ __global__ __launch_bounds__(kRleThreads) __attribute__((amdgpu_waves_per_eu(4))
 // preceding it (bits 24-31): after sorting, that byte IS the BWT output
 // column, so the MTF stage reads it in sorted order without a gather.
 constexpr uint32_t kIdxMask = 0x00FFFFFFu;
+#ifndef LFM_BWT_PACK
+#define LFM_BWT_PACK 0  // 1: bwt_chunk_sort sorts (key - min) << LJ | slot keys only where the range allows (measured no faster)
+#endif
 constexpr uint32_t kKeyBytes = 8;  // first-round key: the 8-byte prefix (0.02 % of rotations tie on symbols)
 
 // First round: every rotation by its 8-byte prefix, in two steps.
@@ -1126,31 +1129,92 @@ __global__ __launch_bounds__(TH) void bwt_chunk_sort(Batch B, const uint32_t* __
     if (c >= nch) return;
     static_assert(IPT == 2 || IPT == 4 || IPT == 8, "flags are packed 2, 4 or 8 per thread");
     using Sort = rocprim::block_sort<uint64_t, TH, IPT, uint32_t, rocprim::block_sort_algorithm::merge_sort>;
+    using SortK = rocprim::block_sort<uint64_t, TH, IPT, rocprim::empty_type, rocprim::block_sort_algorithm::merge_sort>;
     using ExK = rocprim::block_exchange<uint64_t, TH, IPT>;
     using ExV = rocprim::block_exchange<uint32_t, TH, IPT>;
-    constexpr uint32_t NI = TH * IPT;
+    constexpr uint32_t NI = TH * IPT, NW = TH / 64;
     struct Xch {
         uint64_t first[TH], last[TH];
         uint32_t sv[NI];
         uint8_t fl[NI];
     };
+    struct Packed {
+        typename SortK::storage_type s;
+        uint32_t sv[NI];  // the values by load slot
+    };
     __shared__ union alignas(16) {
         typename Sort::storage_type s;
         typename ExK::storage_type ek;
         typename ExV::storage_type ev;
+        Packed pk;
         Xch x;
     } sm;
     const uint32_t cb = cbp[c], ce = cep[c], m = ce - cb, t = threadIdx.x;
     uint64_t k[IPT];
     uint32_t v[IPT];
     chunk_load<TH, IPT>(B, cb, m, t, k, v);
-    // the sort's valid-item count refers to the blocked arrangement
-    ExK().striped_to_blocked(k, k, sm.ek);
-    __syncthreads();
-    ExV().striped_to_blocked(v, v, sm.ev);
-    __syncthreads();
-    Sort().sort(k, v, sm.s, m);
-    __syncthreads();
+    bool packed = false;
+#if LFM_BWT_PACK
+    // Keys only when they fit: the chunk's key range below 2^(64 - LJ), LJ
+    // the bits of a load slot j < m, sorts (k - kmin) << LJ | j as one 64-bit
+    // key (a third less to move per merge step than key + value; slots past m
+    // get ~0, above every packed key, so the whole tile is sorted without a
+    // valid count or a striped-to-blocked exchange); the values come back
+    // through LDS by slot.
+    {
+        __shared__ uint64_t wlo[NW], whi[NW];
+        uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+        for (int q = 0; q < IPT; ++q)
+            if (q * TH + t < m) {
+                lo = min(lo, k[q]);
+                hi = max(hi, k[q]);
+            }
+        for (int d = 32; d > 0; d >>= 1) {
+            lo = min(lo, (uint64_t)__shfl_xor(lo, d));
+            hi = max(hi, (uint64_t)__shfl_xor(hi, d));
+        }
+        if ((t & 63) == 0) {
+            wlo[t >> 6] = lo;
+            whi[t >> 6] = hi;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t x = 0; x < NW; ++x) {
+            lo = min(lo, wlo[x]);
+            hi = max(hi, whi[x]);
+        }
+        const uint32_t LJ = 32u - (uint32_t)__builtin_clz(max(m, 2u) - 1u);
+        if (((hi - lo) >> (64u - LJ)) == 0) {
+            packed = true;
+#pragma unroll
+            for (int q = 0; q < IPT; ++q) {
+                const uint32_t j = q * TH + t;
+                if (j < m) sm.pk.sv[j] = v[q];
+                k[q] = j < m ? ((k[q] - lo) << LJ) | j : ~0ull;
+            }
+            SortK().sort(k, sm.pk.s);
+            __syncthreads();
+            const uint64_t jm = (1ull << LJ) - 1ull;
+#pragma unroll
+            for (int q = 0; q < IPT; ++q) {
+                const uint32_t pos = t * IPT + q;
+                v[q] = pos < m ? sm.pk.sv[(uint32_t)(k[q] & jm)] : 0u;
+                k[q] >>= LJ;  // (the tie flags compare these; positions >= m are never compared)
+            }
+            __syncthreads();
+        }
+    }
+#endif
+    if (!packed) {
+        // the sort's valid-item count refers to the blocked arrangement
+        ExK().striped_to_blocked(k, k, sm.ek);
+        __syncthreads();
+        ExV().striped_to_blocked(v, v, sm.ev);
+        __syncthreads();
+        Sort().sort(k, v, sm.s, m);
+        __syncthreads();
+    }
     sm.x.first[t] = k[0];
     sm.x.last[t] = k[IPT - 1];
     __syncthreads();

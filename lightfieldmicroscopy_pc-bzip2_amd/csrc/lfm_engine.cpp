@@ -487,6 +487,7 @@ Encoder::~Encoder()
             if (hs) (void)hipHostFree(hs);
         if (ev0_) (void)hipEventDestroy(ev0_);
         if (ev1_) (void)hipEventDestroy(ev1_);
+        if (caller_ev_) (void)hipEventDestroy(caller_ev_);
         if (stream_) (void)hipStreamDestroy(stream_);
         if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     }
@@ -545,6 +546,7 @@ int Encoder::submit(const void* img, bool dev, klb_image_header& h, int threads,
 {
     static const SlabSpec whole;
     if (threads <= 0) threads = default_threads();
+    if (int rc = after_caller(dev)) return rc;
     const int p = par_;
     Inflight& f = fly_[p];
     if (f.th.joinable()) f.th.join();  // the encode before last used this buffer set
@@ -1490,6 +1492,26 @@ int normalize_header(klb_image_header& h)
 }
 
 // selection for submit: on the slab's select_frame, else on frame 0 of the image
+// A device input was written by the caller's kernels, typically on the null
+// stream (torch's default stream, lfm_hip_synth without a stream); the
+// encoder's streams are non-blocking, so they would not wait for that work:
+// the encoder's stream waits for an event recorded on the null stream.  (A
+// producer on another stream must be synchronised by the caller; the Python
+// binding does that for torch's current stream.)
+int Encoder::after_caller(bool dev)
+{
+    if (!dev) return 0;
+    if (int rc = ensure_gpu()) return rc;
+    (void)hipSetDevice(device_);
+    if (!caller_ev_ && hipEventCreateWithFlags(&caller_ev_, hipEventDisableTiming) != hipSuccess) {
+        caller_ev_ = nullptr;
+        return 3;
+    }
+    return hipEventRecord(caller_ev_, nullptr) == hipSuccess && hipStreamWaitEvent(stream_, caller_ev_, 0) == hipSuccess
+               ? 0
+               : 3;
+}
+
 int Encoder::preselect(const void* img, bool dev, const klb_image_header& h, const SlabSpec& slab, int* k,
                        float ent[8])
 {
@@ -1545,6 +1567,7 @@ int Encoder::encode_set(const void* img, bool dev, klb_image_header& h, Sink& si
         level = bzip2_level(nominal);
     }
     if (int rc = normalize_header(h)) return rc;
+    if (int rc = after_caller(dev)) return rc;
     const uint8_t* sym = nullptr;
     const uint8_t* dsym = nullptr;
     const bool gpu_bz = use_gpu_bzip2(h, dev);

@@ -226,6 +226,7 @@ private:
                    const SlabSpec* slab, int set);
     int preselect(const void* img, bool dev, const klb_image_header& h, const SlabSpec& slab, int* k, float ent[8]);
     int ensure_gpu();
+    int after_caller(bool dev);
     void* dev_alloc(void*& p, size_t& cap, size_t need);
     void join_inflight();
     Inflight fly_[2];                         // by buffer set
@@ -238,6 +239,7 @@ private:
     bool gpu_ready_ = false;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    hipEvent_t caller_ev_ = nullptr;          // the null stream's work before a device input
     void* d_in_ = nullptr;  size_t d_in_cap_ = 0;
     void* d_sym_[2] = {nullptr, nullptr}; size_t d_sym_cap_[2] = {0, 0};  // by buffer set
     void* d_ws_ = nullptr;  size_t d_ws_cap_ = 0;

@@ -329,6 +329,12 @@ class Encoder:
                     raise LfmError("unsupported tensor dtype %s" % img.dtype)
                 if data_type is not None and data_type != kt and not (data_type == 1 and kt in (1, 5)):
                     raise LfmError("data_type %d does not match tensor dtype %s" % (data_type, img.dtype))
+                # the library orders its reads after the null stream's work
+                # (torch's default stream); a producer on another current
+                # stream is waited for here
+                cur = torch.cuda.current_stream(img.device)
+                if cur != torch.cuda.default_stream(img.device):
+                    cur.synchronize()
                 shape = list(img.shape)
                 while len(shape) < 5:
                     shape = [1] + shape

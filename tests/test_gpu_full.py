@@ -113,7 +113,10 @@ def test_config5_far_volume(lfmlib, gpu, t):
     """t-volume 50 / 99 of the 100-volume config-5 stack (4096 x 4096 x 32,
     video, tiles): coded alone with the predictor chosen on volume 0's frame 0
     (request 8 + k, video bit) its block streams equal the oracle's per-volume
-    digest (cfg5far), and the GPU decode returns every pixel."""
+    digest (cfg5far), and the GPU decode returns every pixel.  No synchronise
+    between the generator (null stream) and the encode, on purpose: the
+    encoder orders its reads of a device input after the null stream's work
+    (Encoder::after_caller; without it this test failed now and then)."""
     e = _full("cfg5far_4096x4096x32x1x100_video_tiles_auto")
     X, Y, Z = e["xyzct"][:3]
     want = e["volumes"][str(t)]
