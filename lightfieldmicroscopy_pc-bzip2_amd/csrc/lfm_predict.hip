@@ -1260,12 +1260,18 @@ static bool fast_ok(const FrameSet& p, int force_generic)
 // one 512-pixel strip, 4 compute waves, 3 steps ahead; the tiles formulas
 // (shifted sums, 32-bit) need more waves per CU to hide their VALU chains:
 // 1024-pixel strips, 8 compute waves (0.227 vs 0.251 ms, round-2 ring 0.236).
+#ifndef LFM_VEC_PD
+#define LFM_VEC_PD 3  // steps of prefetch, angle / space
+#endif
+#ifndef LFM_VEC_NCW
+#define LFM_VEC_NCW 4  // compute waves, angle / space
+#endif
 template <int FAM>
 struct VecShape {
     static constexpr int WPR = FAM == 0 ? 2 : 1;
-    static constexpr int NCW = FAM == 0 ? 8 : 4;
+    static constexpr int NCW = FAM == 0 ? 8 : LFM_VEC_NCW;
     static constexpr int RPW = 1;
-    static constexpr int PD = 3;
+    static constexpr int PD = FAM == 0 ? 3 : LFM_VEC_PD;
 };
 
 template <int FAM, int K, int T, int WPR, int NCW, int RPW, int PD>
