@@ -2037,16 +2037,26 @@ bool sdma_staged_d2h(void* h_dst, const void* d_src, size_t n, int threads, Stag
     auto wait = [&](int b) {
         return hsa_signal_wait_scacquire(sig[b], HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, sdma_wait_state()) == 0;
     };
+    static const bool timing = env_int("LFM_DECODE_TIMING", 0) != 0;
+    double t_wait = 0, t_copy = 0;
+    auto now = [] { return std::chrono::steady_clock::now(); };
     bool ok = issue(0);
     for (size_t i = 0; ok && i < nc; ++i) {
         const int b = (int)(i & 1);
         if (i + 1 < nc) ok = issue(i + 1);
+        auto t0 = now();
         if (!wait(b)) ok = false;
         if (!ok) break;
+        auto t1 = now();
         const size_t off = i * Staging::kChunk, len = std::min(Staging::kChunk, n - off);
         par_memcpy_impl((uint8_t*)h_dst + off, S.buf[b], len, threads);
+        t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        t_copy += std::chrono::duration<double, std::milli>(now() - t1).count();
     }
     for (int b = 0; b < 2; ++b) (void)wait(b);  // nothing still writes a chunk
+    if (timing)
+        std::fprintf(stderr, "sdma d2h: %zu bytes, host copies %.2f ms, waits %.2f ms, %d threads\n", n, t_copy, t_wait,
+                     threads);
     hsa_signal_destroy(sig[0]);
     hsa_signal_destroy(sig[1]);
     S.used[0] = S.used[1] = false;
@@ -2464,7 +2474,11 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                         drc = 3;
                         return;
                     }
-            if ((!sdma_staged_d2h(img + o0, src, n, threads, DB.down) &&
+            // the device -> pinned copies: the runtime's (LFM_DECODE_D2H=1,
+            // default: 57 GB/s, bench decode 55-57 ms) or an SDMA engine's
+            // (0: 28 GB/s, the decode 62-64 ms; profiles/r06_ab_decode_d2h.jsonl)
+            static const int d2h_mode = env_int("LFM_DECODE_D2H", 1);
+            if (((d2h_mode == 1 || !sdma_staged_d2h(img + o0, src, n, threads, DB.down)) &&
                  (!staged_d2h(img + o0, src, n, st, threads, DB.down) || hipStreamSynchronize(st) != hipSuccess))) {
                 drc = 3;
                 return;
