@@ -2136,8 +2136,15 @@ struct DecodeBuffers {
         if (hipGetDevice(&d) != hipSuccess) return false;
         if (dev != d) {
             release();
+            // LFM_DECODE_PRIO=1: slot 0's stream at the highest priority, the
+            // others at the lowest, so the first chunk finishes (and its
+            // download starts) while the second one still decodes
+            static const bool prio = env_int("LFM_DECODE_PRIO", 0) != 0;
+            int least = 0, greatest = 0;
+            if (prio) (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
             for (int k = 0; k < kSlots; ++k)
-                if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) {
+                if ((prio ? hipStreamCreateWithPriority(&st[k], hipStreamNonBlocking, k == 0 ? greatest : least)
+                          : hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking)) != hipSuccess) {
                     release();
                     return false;
                 }
