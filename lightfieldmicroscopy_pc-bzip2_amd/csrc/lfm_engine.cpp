@@ -2099,6 +2099,7 @@ struct DecodeBuffers {
     enum { PAY, SYM, OUT, WS0, BLK0 = WS0 + kSlots, N = BLK0 + kSlots };
     int dev = -1;
     hipStream_t st[kSlots] = {};
+    hipStream_t dl = nullptr;                // the downloads' device -> pinned copies
     void* p[N] = {};
     size_t cap[N] = {};
     uint32_t* hs[kSlots] = {};  // pinned: lens then flags, per slot
@@ -2127,6 +2128,8 @@ struct DecodeBuffers {
             if (st[k]) (void)hipStreamDestroy(st[k]);
             st[k] = nullptr;
         }
+        if (dl) (void)hipStreamDestroy(dl);
+        dl = nullptr;
         down.release();
         dev = -1;
     }
@@ -2148,6 +2151,10 @@ struct DecodeBuffers {
                     release();
                     return false;
                 }
+            if (hipStreamCreateWithFlags(&dl, hipStreamNonBlocking) != hipSuccess) {
+                release();
+                return false;
+            }
             dev = d;
         }
         return true;
@@ -2466,7 +2473,9 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
             frames(c, f0, f1);
             const size_t o0 = f0 * frame_bytes, n = (f1 - f0) * frame_bytes;
             const uint8_t* src = (const uint8_t*)(predicted ? d_out : d_sym) + o0;
-            hipStream_t st = DB.st[c % nslot];
+            // (its own stream: on the chunk's slot stream the copies would
+            // queue behind the kernels of chunk c + nslot, issued meanwhile)
+            hipStream_t st = DB.dl;
             if (hipEventSynchronize(cev[c]) != hipSuccess) {
                 drc = 3;
                 return;
@@ -2481,11 +2490,16 @@ static int gpu_decode(const uint8_t* payload, size_t len, const klb_image_header
                         drc = 3;
                         return;
                     }
-            // the device -> pinned copies: the runtime's (LFM_DECODE_D2H=1,
-            // default: 57 GB/s, bench decode 55-57 ms) or an SDMA engine's
-            // (0: 28 GB/s, the decode 62-64 ms; profiles/r06_ab_decode_d2h.jsonl)
+            // the device -> pinned copies: the runtime's (57 GB/s) or an SDMA
+            // engine's (28 GB/s).  The runtime's copies slow the kernels of
+            // chunks still decoding (config 5, 8 chunks: 403-427 vs 325-349
+            // ms), so LFM_DECODE_D2H=1 (default) takes them only for the last
+            // nslot chunks, whose downloads are the decode's exposed tail
+            // (config 3: 55-57 vs 62-64 ms); 2: always, 0: never
+            // (profiles/r06_ab_decode_d2h*.jsonl)
             static const int d2h_mode = env_int("LFM_DECODE_D2H", 1);
-            if (((d2h_mode == 1 || !sdma_staged_d2h(img + o0, src, n, threads, DB.down)) &&
+            const bool rt = d2h_mode == 2 || (d2h_mode == 1 && c + nslot >= nch);
+            if (((rt || !sdma_staged_d2h(img + o0, src, n, threads, DB.down)) &&
                  (!staged_d2h(img + o0, src, n, st, threads, DB.down) || hipStreamSynchronize(st) != hipSuccess))) {
                 drc = 3;
                 return;
