@@ -756,7 +756,7 @@ def main():
     # the newest PMC traffic file of the kernel (rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE passes over scripts/encode_probe.py, scripts/pmc_summary.py)
     tpath = None
-    for name in ("r05_traffic_predict.json", "r04_traffic_predict.json", "r03_traffic_predict.json"):
+    for name in ("r06_traffic_predict.json", "r05_traffic_predict.json", "r04_traffic_predict.json", "r03_traffic_predict.json"):
         tpath = os.path.join(REPO, "profiles", name)
         if os.path.exists(tpath):
             break
