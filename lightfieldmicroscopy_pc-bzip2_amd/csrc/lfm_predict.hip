@@ -1266,11 +1266,14 @@ static bool fast_ok(const FrameSet& p, int force_generic)
 #ifndef LFM_VEC_NCW
 #define LFM_VEC_NCW 4  // compute waves, angle / space
 #endif
+#ifndef LFM_VEC_RPW
+#define LFM_VEC_RPW 1  // rows per compute wave and step, angle / space
+#endif
 template <int FAM>
 struct VecShape {
     static constexpr int WPR = FAM == 0 ? 2 : 1;
     static constexpr int NCW = FAM == 0 ? 8 : LFM_VEC_NCW;
-    static constexpr int RPW = 1;
+    static constexpr int RPW = FAM == 0 ? 1 : LFM_VEC_RPW;
     static constexpr int PD = FAM == 0 ? 3 : LFM_VEC_PD;
 };
 
