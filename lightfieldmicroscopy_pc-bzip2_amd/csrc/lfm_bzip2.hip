@@ -2279,10 +2279,15 @@ __device__ __forceinline__ uint64_t wave_or_scan_excl(uint64_t x)
     return ((uint64_t)wave_or_scan_excl32((uint32_t)(x >> 32)) << 32) | wave_or_scan_excl32((uint32_t)x);
 }
 
+#ifndef LFM_MTF_BALLOT
+#define LFM_MTF_BALLOT 0  // 1: mtf_win's match masks by eight ballots instead of LDS atomicOr (measured slower)
+#endif
 __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const int32_t* __restrict__ seg_last)
 {
     __shared__ int32_t key[4][256];
+#if !LFM_MTF_BALLOT
     __shared__ uint64_t mt[4][256];
+#endif
     __shared__ uint8_t Pt[4][256], Lt[4][256], inw[4][256];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t s = blockIdx.y, k = blockIdx.x * 4 + wave;
@@ -2324,11 +2329,24 @@ __global__ __launch_bounds__(256) void mtf_win(Batch B, uint32_t nseg_max, const
         const uint32_t c = valid ? cn : 0u;
         cn = llbuf[min(j + 64, je - 1)];
         // match mask of c in this window
+#if LFM_MTF_BALLOT
+        // eight ballots, one per bit of c: the lanes whose byte equals this
+        // lane's (VALU and scalar masks only; the LDS atomicOr per lane
+        // serialised on the long runs of one byte in the BWT output)
+        uint64_t M = ballot64(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int32_t e = (int32_t)(c << (31 - b)) >> 31;  // 0 / -1
+            M &= ~(ballot64(e != 0) ^ (uint64_t)(int64_t)e);
+        }
+        M = valid ? M : 0ull;
+#else
         if (valid) mt[wave][c] = 0;
         wsync();
         if (valid) atomicOr((unsigned long long*)&mt[wave][c], 1ull << lane);
         wsync();
         const uint64_t M = valid ? mt[wave][c] : 0ull;
+#endif
         const uint64_t before = M & lt;
         const bool has_prev = before != 0ull;
         const uint32_t p_in = has_prev ? 63u - (uint32_t)__clzll(before) : 0u;
